@@ -1,0 +1,251 @@
+"""Benchmark: batched exact cosine top-k search (better-search-rag-rust's search hot path).
+
+Workload (BASELINE.json configs[1] per GPU): every rank holds a 1M-row shard of a synthetic
+768-d U(-1,1) f32 corpus (the shard is interval_by_rank(rank, N, N*1M) of one global corpus
+generated on the device), 1000 queries (query 0 = corpus row 0, the reference's self-query),
+top-10.  One step = parallel_top_k_similarity_search for the whole query batch: local search
+on every GPU (bf16 MFMA filter + exact f32 rescore), RCCL all-gather of the partial lists,
+host merge on rank 0.  Weak scaling: the corpus grows with N (1M rows per GPU); `value`
+counts each query once per 1M-row shard, so at N=1 it is plain queries/s over 1M vectors.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "better-search-rag-rust_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+PEAK_BF16_DENSE = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
+PEAK_HBM = 8.0e12          # MI355X HBM3E (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--queries", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--p50-iters", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle (rank 0, N=1)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import bsr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap + timing only
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+
+    D, Q, K = args.dim, args.queries, args.k
+    n_total = args.rows_per_gpu * world
+    iv = bsr.interval_by_rank(rank, world, n_total)
+    start, n_local = iv.start_index, iv.get_count()
+
+    # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index.
+    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE)
+    shard = torch.empty((max(n_local, 1), D), dtype=torch.float32, device=dev)
+    if n_local:
+        bsr.synth_uniform(shard.data_ptr(), start, n_local, D, 42)
+    torch.cuda.synchronize()
+    index.load(shard[:n_local] if n_local else np.zeros((0, D), np.float32), start)
+    del shard
+    torch.cuda.empty_cache()
+
+    # Queries: row 0 of the global corpus (self-query) + seed-43 rows; resident in HBM.
+    qdev = torch.empty((Q, D), dtype=torch.float32, device=dev)
+    bsr.synth_uniform(qdev.data_ptr(), 0, Q, D, 43)
+    bsr.synth_uniform(qdev[0:1].data_ptr(), 0, 1, D, 42)
+    torch.cuda.synchronize()
+
+    comm = None
+    if world > 1:
+        uid = [bsr.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = bsr.Comm(uid[0], rank, world, local_rank)
+
+    lib = bsr.lib()
+    oi = np.empty((Q, K), np.uint64)
+    od = np.empty((Q, K), np.float32)
+    oc = np.empty(Q, np.uint32)
+    comm_h = comm._h if comm else None
+
+    def step(nq=Q, qptr=None):
+        st = lib.bsr_parallel_top_k_similarity_search(comm_h, index._h, qptr or qdev.data_ptr(), nq, K,
+                                                       oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+        if st != 0:
+            raise bsr.BsrError(st, lib.bsr_last_error().decode())
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    index.profile(reset=True)
+    stats_fb = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stats_fb += index.last_stats().n_fallback
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = index.profile(reset=True)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    st = index.last_stats()
+
+    # Self-query check of the reference's driver (src/main.rs:141-154): row 0 ranks first.
+    self_ok = None
+    if rank == 0:
+        self_ok = bool(oi[0, 0] == 0 and od[0, 0] == 0.0)
+
+    # p50 single-query latency (config 4 style path: exact HBM-bound scan), all ranks.
+    lat = []
+    for _ in range(args.p50_iters):
+        barrier()
+        t1 = time.perf_counter()
+        step(1, qdev[1:2].data_ptr())
+        lat.append((time.perf_counter() - t1) * 1e3)
+    p50 = statistics.median(lat) if lat else None
+    prof_scan = index.profile(reset=True)
+
+    out = None
+    if rank == 0:
+        launches = max(prof.gemm_emit_launches, 1)
+        emit_ms = prof.gemm_emit_ms / launches
+        flops = 2.0 * Q * n_local * D
+        achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                pm = json.load(open(args.pmc_json))
+                if pm.get("rows") == n_local and pm.get("queries") == Q:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        value = Q * world / (ms_per_step * 1e-3)
+        out = {
+            "metric": "queries/sec + p50 latency, 768-d top-10 over N vectors @1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic U(-1,1) f32 corpus generated on device (seed 42), 1000 queries (seed 43, query 0 = row 0)",
+            "config": {
+                "workload": f"configs[1] per GPU: {n_local} x {D} f32 rows per GPU ({n_total} total), "
+                            f"{Q} batched queries, top-{K}; value = queries x 1M-row shards / s",
+                "rows_total": n_total, "rows_per_gpu": n_local, "queries": Q, "top_k": K, "dim": D,
+                "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank) + RCCL all-gather",
+                "filter": "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates, exact sequential-f32 rescore",
+                "qps_over_full_corpus": round(Q / (ms_per_step * 1e-3), 2),
+            },
+            "p50_ms": round(p50, 4) if p50 is not None else None,
+            "p50_config": f"1 query over {n_total} rows (exact scan, HBM-bound)",
+            "roofline": {
+                "bound": "mfma", "kernel": "k_gemm_filter<emit>",
+                "achieved": round(achieved, 2) if achieved else None,
+                "peak": PEAK_BF16_DENSE / 1e12, "unit": "TFLOP/s",
+                "frac": round(achieved * 1e12 / PEAK_BF16_DENSE, 4) if achieved else None,
+                "traffic": traffic,
+                "algorithmic_flops_per_launch": flops,
+                "avg_launch_ms": round(emit_ms, 5),
+            },
+            "kernels_ms_per_step": {
+                "gemm_emit": round(prof.gemm_emit_ms / args.steps, 4),
+                "gemm_sample": round(prof.gemm_sample_ms / args.steps, 4),
+                "select": round(prof.select_ms / args.steps, 4),
+                "rescore": round(prof.rescore_ms / args.steps, 4),
+                "scan_fallback": round(prof.scan_ms / args.steps, 4),
+                "local_search_total": round(prof.search_ms / args.steps, 4),
+            },
+            "p50_scan_kernel_ms": round(prof_scan.scan_ms / max(prof_scan.scan_launches, 1), 4),
+            "fallback_queries_per_step": stats_fb / args.steps,
+            "candidates_per_query": st.n_candidates,
+            "self_query_rank1": self_ok,
+        }
+        # HBM roofline of the single-query scan kernel (bytes = N*d*4 per query).
+        scan_ms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)
+        if scan_ms > 0:
+            gbs = n_local * D * 4 / (scan_ms * 1e-3) / 1e9
+            out["roofline_scan"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM / 1e9,
+                                    "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4)}
+
+    # Parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on the same corpus.
+    if rank == 0 and world == 1 and (args.verify or not args.no_cpu_baseline):
+        import oracle
+        rows_h = index.get_many()
+        q_h = qdev.cpu().numpy()
+        if args.verify:
+            nv = min(args.verify, Q)
+            step()  # refresh oi/od for the full batch
+            wi, wd, wc = oracle.parallel_top_k(rows_h, q_h[:nv], K, size=min(16, os.cpu_count() or 1),
+                                               threads=min(16, os.cpu_count() or 1))
+            out["parity_spot_check"] = {
+                "queries": nv,
+                "indices_equal": bool(np.array_equal(oi[:nv], wi)),
+                "distance_bits_equal": bool(np.array_equal(od[:nv].view(np.uint32), wd.view(np.uint32))),
+            }
+        if not args.no_cpu_baseline:
+            threads = max(1, min(16, os.cpu_count() or 1))
+            t1 = time.perf_counter()
+            oracle.parallel_top_k(rows_h, q_h[1:2], K, size=threads, threads=threads)
+            one = time.perf_counter() - t1
+            nq_cpu = max(1, min(Q, int(args.cpu_seconds / max(one, 1e-3))))
+            t1 = time.perf_counter()
+            oracle.parallel_top_k(rows_h, q_h[:nq_cpu], K, size=threads, threads=threads)
+            cpu_t = time.perf_counter() - t1
+            out["cpu_baseline"] = {
+                "value": round(nq_cpu / cpu_t, 4), "unit": "queries/s", "cores": threads, "kind": "port",
+                "sample": f"{nq_cpu} of the {Q} queries over the same {n_local}-row corpus, "
+                          f"{threads} rank threads (mpiexec analogue), oracle/bsr_oracle.c",
+            }
+        else:
+            out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    barrier()
+    if comm:
+        comm.close()
+    index.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

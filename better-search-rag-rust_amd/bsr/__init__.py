@@ -1,0 +1,440 @@
+"""Host-side mirror of better-search-rag-rust's search-path interface over the C ABI.
+
+Every function here is a thin ctypes call into ``lib/libbsr.so`` (include/bsr.h); the
+compute runs in the gfx950 HIP kernels.  There is no CPU fallback: if the library or a GPU
+is missing the calls raise :class:`BsrError`.  Names and argument meaning follow the
+reference (paths relative to nichmorgan/better-search-rag-rust):
+
+=====================================  ===============================================
+``cosine_distance(a, b)``              src/metrics.rs:143-165
+``interval_by_rank(rank, size, n)``    src/mpi_helpers/load_balance.rs:24-42
+``Index`` (get_count/get_many/get)     src/vectorstore/polars.rs:79-169,243-246
+``compute_local_top_k``                src/mpi_helpers/metrics.rs:16-53
+``gather_top_k_results``               src/mpi_helpers/metrics.rs:56-138
+``compute_global_top_k``               src/mpi_helpers/metrics.rs:141-171
+``parallel_top_k_similarity_search``   src/mpi_helpers/metrics.rs:174-206
+``calculate_accuracy_metrics``         src/mpi_helpers/metrics.rs:217-249
+=====================================  ===============================================
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr.so")
+
+BSR_OK = 0
+BSR_F32 = 0
+BSR_BF16 = 1
+BSR_MAX_K = 256
+BSR_FLAG_EXACT_ONLY = 1
+BSR_FLAG_PROFILE = 2
+ROOT = 0  # src/mpi_helpers/mod.rs:8
+
+
+class BsrError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{_status_name(status)}: {message}")
+        self.status = status
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_uint32), ("dtype", ctypes.c_uint32), ("max_k", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+class _Interval(ctypes.Structure):
+    _fields_ = [("start_index", ctypes.c_uint64), ("end_index", ctypes.c_uint64)]
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("n_queries", ctypes.c_uint32), ("n_exact_direct", ctypes.c_uint32),
+                ("n_fallback", ctypes.c_uint32), ("n_candidates", ctypes.c_uint32),
+                ("n_emitted", ctypes.c_uint64)]
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [("gemm_emit_ms", ctypes.c_double), ("gemm_emit_launches", ctypes.c_uint64),
+                ("gemm_sample_ms", ctypes.c_double), ("gemm_sample_launches", ctypes.c_uint64),
+                ("select_ms", ctypes.c_double), ("select_launches", ctypes.c_uint64),
+                ("rescore_ms", ctypes.c_double), ("rescore_launches", ctypes.c_uint64),
+                ("scan_ms", ctypes.c_double), ("scan_launches", ctypes.c_uint64),
+                ("search_ms", ctypes.c_double), ("searches", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_lib = None
+_P = ctypes.c_void_p
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbsr.so (raises if it has not been built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BsrError(-3, f"{LIB_PATH} not built (run __graft_entry__.build()); no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    u32, u64, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    sig = {
+        "bsr_last_error": (ctypes.c_char_p, []),
+        "bsr_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+        "bsr_version": (ctypes.c_char_p, []),
+        "bsr_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "bsr_cosine_distance": (ctypes.c_int, [_P, u32, _P, u32, ctypes.POINTER(ctypes.c_float)]),
+        "bsr_interval_by_rank": (ctypes.c_int, [i32, i32, u64, ctypes.POINTER(_Interval)]),
+        "bsr_index_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.POINTER(_P)]),
+        "bsr_index_destroy": (None, [_P]),
+        "bsr_index_load": (ctypes.c_int, [_P, _P, u64, u64]),
+        "bsr_index_append": (ctypes.c_int, [_P, _P, u64]),
+        "bsr_index_count": (ctypes.c_int, [_P, ctypes.POINTER(u64)]),
+        "bsr_index_global_offset": (ctypes.c_int, [_P, ctypes.POINTER(u64)]),
+        "bsr_index_get_many": (ctypes.c_int, [_P, u64, u64, _P]),
+        "bsr_local_top_k": (ctypes.c_int, [_P, _P, u32, u32, _P, _P, _P]),
+        "bsr_global_top_k": (ctypes.c_int, [_P, _P, _P, u32, u32, u32, u32, _P, _P, _P]),
+        "bsr_comm_unique_id": (ctypes.c_int, [_P]),
+        "bsr_comm_init": (ctypes.c_int, [_P, i32, i32, i32, ctypes.POINTER(_P)]),
+        "bsr_comm_destroy": (None, [_P]),
+        "bsr_comm_rank": (ctypes.c_int, [_P, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "bsr_gather_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
+        "bsr_parallel_top_k_similarity_search": (ctypes.c_int, [_P, _P, _P, u32, u32, _P, _P, _P]),
+        "bsr_index_last_stats": (ctypes.c_int, [_P, ctypes.POINTER(SearchStats)]),
+        "bsr_index_profile": (ctypes.c_int, [_P, ctypes.POINTER(Profile), ctypes.c_int]),
+        "bsr_synth_uniform": (ctypes.c_int, [_P, u64, u64, u32, u64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _status_name(s: int) -> str:
+    try:
+        return lib().bsr_status_string(s).decode()
+    except Exception:  # library missing
+        return f"status {s}"
+
+
+def _check(status: int):
+    if status != BSR_OK:
+        raise BsrError(status, lib().bsr_last_error().decode())
+
+
+def _ptr(a) -> Optional[int]:
+    """Data pointer of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    raise TypeError(f"unsupported buffer type {type(a)}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().bsr_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def version() -> str:
+    return lib().bsr_version().decode()
+
+
+# ---- a-1 --------------------------------------------------------------------------------
+def cosine_distance(a, b) -> float:
+    """src/metrics.rs:143-165 (a = stored row, b = query), computed on the GPU."""
+    a = np.ascontiguousarray(a, np.float32).ravel()
+    b = np.ascontiguousarray(b, np.float32).ravel()
+    out = ctypes.c_float(0.0)
+    _check(lib().bsr_cosine_distance(_ptr(a) if a.size else None, a.size,
+                                     _ptr(b) if b.size else None, b.size, ctypes.byref(out)))
+    return float(np.float32(out.value))
+
+
+# ---- a-3 --------------------------------------------------------------------------------
+@dataclass
+class RankInterval:
+    """src/mpi_helpers/load_balance.rs:8-17."""
+    start_index: int
+    end_index: int
+
+    def get_count(self) -> int:
+        # The reference's release build wraps end - start when end < start and then slices
+        # nothing; the effective count is therefore max(0, end - start).
+        return max(0, self.end_index - self.start_index)
+
+
+def interval_by_rank(rank: int, size: int, count: int) -> RankInterval:
+    out = _Interval()
+    _check(lib().bsr_interval_by_rank(rank, size, count, ctypes.byref(out)))
+    return RankInterval(out.start_index, out.end_index)
+
+
+@dataclass
+class SliceArgs:
+    """src/vectorstore/polars.rs:12-15."""
+    offset: int
+    length: int
+
+
+# ---- the rank's shard ---------------------------------------------------------------------
+class Index:
+    """One rank's corpus block resident in HBM (read side of PolarsVectorstore)."""
+
+    def __init__(self, dim: int = 768, max_k: int = 64, device: int = -1, dtype: int = BSR_F32,
+                 flags: int = 0):
+        cfg = _Config(dim, dtype, max_k, flags, device)
+        h = _P()
+        _check(lib().bsr_index_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.dim = dim
+        self.max_k = max_k
+        self.dtype = dtype
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bsr_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _rows(self, rows):
+        if isinstance(rows, np.ndarray):
+            want = np.uint16 if self.dtype == BSR_BF16 else np.float32
+            rows = np.ascontiguousarray(rows, want)
+            if rows.ndim == 1:
+                rows = rows.reshape(1, -1)
+            n = rows.shape[0]
+            if n and rows.shape[1] != self.dim:
+                raise BsrError(-6, f"row length {rows.shape[1]} != dim {self.dim}")
+            return rows, n
+        n = int(rows.shape[0]) if rows.dim() > 1 else 1
+        return rows, n
+
+    def load(self, rows, global_offset: int = 0):
+        rows, n = self._rows(rows)
+        _check(lib().bsr_index_load(self._h, _ptr(rows) if n else None, n, global_offset))
+        return self
+
+    def append_many(self, rows):
+        """PolarsVectorstore::append_many (src/vectorstore/polars.rs:101-119)."""
+        rows, n = self._rows(rows)
+        _check(lib().bsr_index_append(self._h, _ptr(rows) if n else None, n))
+
+    def append(self, vector):
+        self.append_many(np.asarray(vector).reshape(1, -1))
+
+    def get_count(self) -> int:
+        n = ctypes.c_uint64()
+        _check(lib().bsr_index_count(self._h, ctypes.byref(n)))
+        return n.value
+
+    def global_offset(self) -> int:
+        n = ctypes.c_uint64()
+        _check(lib().bsr_index_global_offset(self._h, ctypes.byref(n)))
+        return n.value
+
+    def get_many(self, slice_args: Optional[SliceArgs] = None) -> np.ndarray:
+        count = self.get_count()
+        if slice_args is None:
+            off, length = 0, count
+        else:
+            off = min(max(slice_args.offset, 0), count)
+            length = min(slice_args.length, count - off)
+        out = np.empty((length, self.dim), np.float32)
+        _check(lib().bsr_index_get_many(self._h, off, length, _ptr(out) if length else None))
+        return out
+
+    def get(self, index: int) -> np.ndarray:
+        rows = self.get_many(SliceArgs(index, 1))
+        if rows.shape[0] == 0:
+            raise BsrError(-1, "Index not found")
+        return rows[0]
+
+    def local_top_k(self, queries, k: int):
+        """Batched compute_local_top_k -> (idx [Q,k] u64, dist [Q,k] f32, count [Q] u32)."""
+        q = np.ascontiguousarray(queries, np.float32)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        if q.shape[1] != self.dim:
+            raise BsrError(-6, f"query length {q.shape[1]} != dim {self.dim}")
+        nq = q.shape[0]
+        oi = np.empty((nq, k), np.uint64)
+        od = np.empty((nq, k), np.float32)
+        oc = np.empty(nq, np.uint32)
+        _check(lib().bsr_local_top_k(self._h, _ptr(q), nq, k, _ptr(oi), _ptr(od), _ptr(oc)))
+        return oi, od, oc
+
+    def local_top_k_device(self, queries, nq: int, k: int, out_idx, out_dist, out_count):
+        """Zero-copy variant on device buffers (torch tensors or raw pointers)."""
+        _check(lib().bsr_local_top_k(self._h, _ptr(queries), nq, k, _ptr(out_idx), _ptr(out_dist),
+                                     _ptr(out_count)))
+
+    def last_stats(self) -> SearchStats:
+        s = SearchStats()
+        _check(lib().bsr_index_last_stats(self._h, ctypes.byref(s)))
+        return s
+
+    def profile(self, reset: bool = False) -> Profile:
+        p = Profile()
+        _check(lib().bsr_index_profile(self._h, ctypes.byref(p), int(reset)))
+        return p
+
+
+# ---- communicator -----------------------------------------------------------------------
+class Comm:
+    """RCCL communicator over the ranks (one process per GPU) -- replaces the MPI world."""
+
+    def __init__(self, unique_id: bytes, rank: int, size: int, device: int = -1):
+        h = _P()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        _check(lib().bsr_comm_init(buf, rank, size, device, ctypes.byref(h)))
+        self._h = h
+        self.rank = rank
+        self.size = size
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        _check(lib().bsr_comm_unique_id(buf))
+        return bytes(buf)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bsr_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- a-2 ... a-6 (reference-shaped, single query) -------------------------------------
+def compute_local_top_k(index: Index, rank: int, size: int, top_k: int, target_vector
+                        ) -> List[Tuple[int, float]]:
+    """src/mpi_helpers/metrics.rs:16-53.  `index` holds this rank's block, loaded with the
+    global offset interval_by_rank(rank, size, N).start_index."""
+    idx, dist, cnt = index.local_top_k(np.asarray(target_vector, np.float32).reshape(1, -1), top_k)
+    return [(int(idx[0, i]), float(dist[0, i])) for i in range(int(cnt[0]))]
+
+
+def compute_global_top_k(global_indices: Sequence[int], global_distances: Sequence[float],
+                         top_k: int) -> List[Tuple[int, float]]:
+    """src/mpi_helpers/metrics.rs:141-171 (stable sort by distance, dedupe, keep top_k)."""
+    gi = np.ascontiguousarray(global_indices, np.uint64).ravel()
+    gd = np.ascontiguousarray(global_distances, np.float32).ravel()
+    n = gi.size
+    cnt = np.array([n], np.uint32)
+    if n == 0:  # keep the pointers valid; the count says there is nothing to read
+        gi, gd = np.zeros(1, np.uint64), np.zeros(1, np.float32)
+    oi = np.empty(max(top_k, 1), np.uint64)
+    od = np.empty(max(top_k, 1), np.float32)
+    oc = np.empty(1, np.uint32)
+    _check(lib().bsr_global_top_k(_ptr(gi), _ptr(gd), _ptr(cnt), 1, 1, max(n, 1), top_k, _ptr(oi),
+                                  _ptr(od), _ptr(oc)))
+    return [(int(oi[i]), float(od[i])) for i in range(int(oc[0]))]
+
+
+def merge_top_k_lists(idx, dist, count, top_k: int):
+    """compute_global_top_k for many queries at once: idx/dist [L,Q,k_in], count [L,Q]."""
+    idx = np.ascontiguousarray(idx, np.uint64)
+    dist = np.ascontiguousarray(dist, np.float32)
+    count = np.ascontiguousarray(count, np.uint32)
+    L, Q, k_in = idx.shape
+    oi = np.empty((Q, top_k), np.uint64)
+    od = np.empty((Q, top_k), np.float32)
+    oc = np.empty(Q, np.uint32)
+    _check(lib().bsr_global_top_k(_ptr(idx), _ptr(dist), _ptr(count), L, Q, k_in, top_k, _ptr(oi),
+                                  _ptr(od), _ptr(oc)))
+    return oi, od, oc
+
+
+def gather_top_k_results(world, rank: int, local_top_k: List[Tuple[int, float]]):
+    """src/mpi_helpers/metrics.rs:56-138: rank-order concatenation at the root.
+
+    `world` is a torch.distributed process group (any backend, e.g. gloo on CPU) or None
+    for a single rank.  Non-root ranks get empty lists, like the reference."""
+    local_idx = [int(i) for i, _ in local_top_k]
+    local_dist = [float(d) for _, d in local_top_k]
+    if world is None:
+        return local_idx, local_dist
+    import torch.distributed as dist
+
+    gathered = [None] * dist.get_world_size(world)
+    dist.all_gather_object(gathered, (local_idx, local_dist), group=world)
+    if rank != ROOT:
+        return [], []
+    gi, gd = [], []
+    for part_idx, part_dist in gathered:  # rank order
+        gi.extend(part_idx)
+        gd.extend(part_dist)
+    return gi, gd
+
+
+def parallel_top_k_similarity_search(world, rank: int, size: int, index: Index, top_k: int,
+                                     target_vector) -> Optional[List[Tuple[int, float]]]:
+    """src/mpi_helpers/metrics.rs:174-206.  With a :class:`Comm` the whole step runs in the
+    native library (RCCL all-gather + host merge); with a torch.distributed group (or None)
+    the gather goes through torch.distributed and the merge through the C ABI."""
+    q = np.asarray(target_vector, np.float32).reshape(1, -1)
+    if isinstance(world, Comm) or world is None:
+        oi = np.empty((1, top_k), np.uint64)
+        od = np.empty((1, top_k), np.float32)
+        oc = np.empty(1, np.uint32)
+        _check(lib().bsr_parallel_top_k_similarity_search(world._h if world else None, index._h, _ptr(q),
+                                                          1, top_k, _ptr(oi), _ptr(od), _ptr(oc)))
+        if rank != ROOT:
+            return None
+        return [(int(oi[0, i]), float(od[0, i])) for i in range(int(oc[0]))]
+    local = compute_local_top_k(index, rank, size, top_k, q[0])
+    gi, gd = gather_top_k_results(world, rank, local)
+    if rank != ROOT:
+        return None
+    return compute_global_top_k(gi, gd, top_k)
+
+
+def calculate_accuracy_metrics(top_k_results, query_idx: int, top_k: int):
+    """src/mpi_helpers/metrics.rs:217-249 (MRR, recall@k, overlap of the query row)."""
+    position = 0
+    for i, (idx, _) in enumerate(top_k_results):
+        if idx == query_idx:
+            position = i + 1
+            break
+    mrr = 1.0 / position if position > 0 else 0.0
+    recall = 1.0 if 0 < position <= top_k else 0.0
+    overlap = 1.0 if position > 0 else 0.0
+    return mrr, recall, overlap
+
+
+def synth_uniform(dev_ptr: int, row0: int, n_rows: int, dim: int, seed: int):
+    """Fill device memory with the synthetic U(-1,1) corpus rows [row0, row0+n_rows)."""
+    _check(lib().bsr_synth_uniform(dev_ptr, row0, n_rows, dim, seed))
+
+
+def synth_uniform_np(row0: int, n_rows: int, dim: int, seed: int) -> np.ndarray:
+    """Host replica of bsr_synth_uniform (splitmix64 of (seed, global element index))."""
+    with np.errstate(over="ignore"):
+        g = (np.uint64(row0) * np.uint64(dim) + np.arange(n_rows * dim, dtype=np.uint64))
+        x = np.uint64(seed) * np.uint64(0xD1B54A32D192ED03) + g
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    v = (x >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 8388608.0) - np.float32(1.0)
+    return v.reshape(n_rows, dim)

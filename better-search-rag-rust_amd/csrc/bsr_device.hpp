@@ -1,0 +1,141 @@
+// bsr_device.hpp -- device-side building blocks shared by the kernels (gfx950, wave64).
+//
+// * Exact distance: the reference's cosine_distance (src/metrics.rs:143-165) finished from
+//   per-lane sequential partial sums.  This translation unit is compiled with
+//   -ffp-contract=off, so `a * b` and `acc + p` round separately exactly like Rust's f32
+//   ops; sqrt uses __builtin_sqrtf (correctly rounded; NB: HIP's __fsqrt_rn lowers to the
+//   approximate native sqrt on ROCm 7.2) and `/` is the correctly rounded division.
+// * Keys: a result (distance d >= 0, local row r) is the u64 (bits(d) << 32) | r, so the
+//   reference's order (distance asc, index asc -- SURVEY.md §8a-5) is plain u64 order.
+// * WaveTopK<E>: a sorted list of the 64*E smallest keys held by one wavefront, position
+//   p = e*64 + lane.  Insertion is wave-parallel (ballot + popcount + one shuffle).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bsr {
+
+constexpr int kWave = 64;
+constexpr uint64_t kKeyNone = ~0ull;
+
+__device__ __forceinline__ uint64_t dist_key(float d, uint32_t row) {
+    return ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)row;
+}
+__device__ __forceinline__ float key_dist(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+__device__ __forceinline__ uint32_t key_row(uint64_t k) { return (uint32_t)k; }
+
+// Score keys order LARGER approximate scores first (then smaller row): the candidate
+// stage keeps the smallest score keys.
+__device__ __forceinline__ uint32_t ord_f32(float s) {
+    uint32_t u = __float_as_uint(s);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ uint64_t score_key(float s, uint32_t row) {
+    return ((uint64_t)(~ord_f32(s)) << 32) | (uint64_t)row;
+}
+__device__ __forceinline__ float score_key_score(uint64_t k) { return unord_f32(~(uint32_t)(k >> 32)); }
+
+// Round-to-nearest-even f32 -> bf16 bits (inputs are finite here).
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float x) {
+    uint32_t u = __float_as_uint(x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// src/metrics.rs:144-164 given the sequential dot product, the max |a_i - b_i| (the
+// identical test `all |a_i-b_i| <= 1e-10` is `max <= 1e-10` for finite inputs) and the two
+// magnitudes (each sqrt of a sequential sum of squares).
+__device__ __forceinline__ float finish_distance(float dot, float maxdiff, float mag_a, float mag_b) {
+    if (maxdiff <= 1e-10f) return 0.0f;                 // :149-151
+    if (mag_a == 0.0f || mag_b == 0.0f) return 1.0f;    // :157-159
+    float denom = mag_a * mag_b;
+    float s = dot / denom;                              // :161
+    s = fmaxf(s, -1.0f);                                // :162 .max(-1.0) (maxNum: NaN -> -1)
+    s = fminf(s, 1.0f);                                 //      .min(1.0)
+    return 1.0f - s;                                    // :164
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x) {
+    int lo = __shfl_up((int)(uint32_t)x, 1, kWave);
+    int hi = __shfl_up((int)(uint32_t)(x >> 32), 1, kWave);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <int E>
+struct WaveTopK {
+    uint64_t v[E];
+
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = kKeyNone;
+    }
+    // Key at (wave-uniform) position pos.
+    __device__ __forceinline__ uint64_t at(int pos) const {
+        const int e = pos >> 6, l = pos & 63;
+        uint64_t x = v[0];
+#pragma unroll
+        for (int i = 1; i < E; ++i)
+            if (i == e) x = v[i];
+        return readlane64(x, l);
+    }
+    // Insert a wave-uniform key (duplicates allowed; the largest entry falls off).
+    __device__ __forceinline__ void insert(uint64_t x) {
+        const int lane = lane_id();
+        int pos = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) pos += __popcll(__ballot(v[e] < x));
+#pragma unroll
+        for (int e = E - 1; e >= 0; --e) {
+            const uint64_t up = shfl_up1_64(v[e]);
+            const uint64_t carry = (e > 0) ? readlane64(v[e > 0 ? e - 1 : 0], 63) : kKeyNone;
+            const uint64_t prev = (lane == 0) ? carry : up;
+            const int p = e * kWave + lane;
+            v[e] = (p > pos) ? prev : ((p == pos) ? x : v[e]);
+        }
+    }
+    // Offer one key per lane (kKeyNone = nothing); keeps the smallest `k` keys seen.
+    // `thr` is the current k-th smallest key, updated.
+    __device__ __forceinline__ void offer(uint64_t x, int k, uint64_t& thr) {
+        uint64_t m = __ballot(x < thr);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint64_t y = readlane64(x, l);
+            if (y < thr) {
+                insert(y);
+                thr = at(k - 1);
+            }
+        }
+    }
+    // Store the first n positions (n <= 64*E) to out[0..n).
+    __device__ __forceinline__ void store(uint64_t* out, int n) const {
+        const int lane = lane_id();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = e * kWave + lane;
+            if (p < n) out[p] = v[e];
+        }
+    }
+};
+
+// splitmix64 finaliser: the counter-based generator behind bsr_synth_uniform.
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+}  // namespace bsr

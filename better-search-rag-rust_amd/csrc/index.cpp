@@ -1,0 +1,462 @@
+// index.cpp -- the rank's corpus shard in HBM and the local search pipeline
+// (compute_local_top_k, src/mpi_helpers/metrics.rs:16-53, for a batch of queries).
+//
+// Pipeline for a batch:
+//   1. query prep          exact |b|, normalised bf16 copy, flags
+//   2. sample filter       bf16 MFMA scores of every 32nd row -> tau0 = ks-th best (per query)
+//   3. emit filter         bf16 MFMA scores of every row; rows with score >= tau0 -> candidates
+//   4. select              top-(k'+1) candidates by approximate score
+//   5. rescore             exact sequential-f32 distances of k' candidates, top-k, certify
+//   6. fallback            exact full scan for any uncertified / ineligible query
+// Small batches, k > 200, or an index with out-of-range norms use the exact scan only.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "internal.hpp"
+#include "kernels.hpp"
+
+namespace bsr {
+
+// Certification bound on |approximate cosine - reference cosine|: two bf16
+// roundings of normalised operands (2u+u^2, u = 2^-8), the f32 accumulation of the MFMA
+// and of the reference (2*gamma_768), f32 magnitudes and the reference's final rounding,
+// with margin.
+constexpr double kEBound = 8.5e-3;
+constexpr uint32_t kMinBatchForFilter = 16;
+constexpr uint32_t kMaxKForFilter = 200;
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+void clear_error() { g_err.clear(); }
+const char* last_error_cstr() { return g_err.c_str(); }
+
+int DevBuf::ensure(size_t need) {
+    if (need <= bytes && p) return BSR_OK;
+    release();
+    if (need == 0) need = 16;
+    hipError_t e = hipMalloc(&p, need);
+    if (e != hipSuccess) {
+        p = nullptr;
+        bytes = 0;
+        (void)hipGetLastError();
+        return set_error(BSR_E_NOMEM, "hipMalloc(%zu bytes) failed: %s", need, hipGetErrorString(e));
+    }
+    bytes = need;
+    return BSR_OK;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+int select_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return set_error(BSR_E_NODEVICE, "no HIP device visible (this engine has no CPU path)");
+    }
+    if (device >= 0) {
+        if (device >= n) return set_error(BSR_E_INVALID, "device %d out of range (%d visible)", device, n);
+        BSR_HIP(hipSetDevice(device));
+    }
+    return BSR_OK;
+}
+
+Events::~Events() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+}
+int Events::create() {
+    if (!a) BSR_HIP(hipEventCreate(&a));
+    if (!b) BSR_HIP(hipEventCreate(&b));
+    return BSR_OK;
+}
+
+}  // namespace bsr
+
+using namespace bsr;
+
+// ---------------------------------------------------------------------------------------
+// profiling helpers
+// ---------------------------------------------------------------------------------------
+static inline bool profiling(const bsr_index* ix) { return (ix->cfg.flags & BSR_FLAG_PROFILE) != 0; }
+static inline void ev_begin(bsr_index* ix, Events& e) {
+    if (profiling(ix) && e.a) { (void)hipEventRecord(e.a, ix->stream); e.armed = true; }
+}
+static inline void ev_end(bsr_index* ix, Events& e) {
+    if (profiling(ix) && e.armed) (void)hipEventRecord(e.b, ix->stream);
+}
+static inline void ev_collect(Events& e, double& ms, uint64_t& n, uint64_t launches) {
+    if (!e.armed) return;
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, e.a, e.b) == hipSuccess) { ms += t; n += launches; }
+    e.armed = false;
+}
+
+// ---------------------------------------------------------------------------------------
+// load / append
+// ---------------------------------------------------------------------------------------
+static int index_prepare_rows(bsr_index* ix, const void* rows, uint64_t n_rows, uint64_t first_row) {
+    // Copy rows [first_row, first_row+n_rows) of the padded slab from the caller's buffer.
+    float* dst = ix->rows.as<float>() + first_row * ix->ld;
+    const bool dev = is_device_ptr(rows);
+    const size_t elem = ix->cfg.dtype == BSR_BF16 ? 2 : 4;
+    const void* src = rows;
+    if (!dev) {
+        BSR_TRY(ix->tmp.ensure(n_rows * (size_t)ix->dim * elem));
+        BSR_HIP(hipMemcpyAsync(ix->tmp.p, rows, n_rows * (size_t)ix->dim * elem, hipMemcpyHostToDevice,
+                               ix->stream));
+        src = ix->tmp.p;
+    }
+    if (ix->cfg.dtype == BSR_BF16)
+        BSR_HIP(launch_widen_bf16_rows(static_cast<const uint16_t*>(src), n_rows, ix->dim, ix->ld, dst, ix->stream));
+    else
+        BSR_HIP(launch_copy_rows_f32(static_cast<const float*>(src), n_rows, ix->dim, ix->ld, dst, ix->stream));
+    return BSR_OK;
+}
+
+static int index_finish_load(bsr_index* ix) {
+    BSR_TRY(ix->na.ensure(ix->n_pad * sizeof(float)));
+    BSR_TRY(ix->cbf.ensure(ix->n_pad * (size_t)ix->ld * 2));
+    BSR_TRY(ix->flags.ensure(sizeof(uint32_t)));
+    BSR_HIP(hipMemsetAsync(ix->flags.p, 0, sizeof(uint32_t), ix->stream));
+    BSR_HIP(hipMemsetAsync(ix->na.p, 0, ix->n_pad * sizeof(float), ix->stream));
+    if (ix->n) BSR_HIP(launch_row_norms(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->na.as<float>(),
+                                        ix->flags.as<uint32_t>(), ix->stream));
+    BSR_HIP(launch_rows_to_bf16n(ix->rows.as<float>(), ix->na.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld,
+                                 ix->cbf.as<uint16_t>(), ix->stream));
+    uint32_t f = 0;
+    BSR_HIP(hipMemcpyAsync(&f, ix->flags.p, sizeof f, hipMemcpyDeviceToHost, ix->stream));
+    BSR_HIP(hipStreamSynchronize(ix->stream));
+    ix->row_flags = f;
+    if (f & kRowNonFinite) {
+        ix->loaded = false;
+        ix->n = 0;
+        return set_error(BSR_E_NONFINITE, "corpus contains NaN/Inf (the reference panics on NaN distances)");
+    }
+    ix->approx_ok = !(f & (kRowNormOvf | kRowNormRange)) && !(ix->cfg.flags & BSR_FLAG_EXACT_ONLY);
+    ix->loaded = true;
+    return BSR_OK;
+}
+
+int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
+    if (!cfg || !out) return set_error(BSR_E_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->dim == 0) return set_error(BSR_E_INVALID, "dim must be >= 1");
+    if (cfg->dtype != BSR_F32 && cfg->dtype != BSR_BF16) return set_error(BSR_E_INVALID, "unknown dtype");
+    if (cfg->max_k == 0 || cfg->max_k > BSR_MAX_K)
+        return set_error(BSR_E_INVALID, "max_k must be in [1, %u]", BSR_MAX_K);
+    BSR_TRY(select_device(cfg->device));
+    bsr_index* ix = new (std::nothrow) bsr_index();
+    if (!ix) return set_error(BSR_E_NOMEM, "host allocation failed");
+    ix->cfg = *cfg;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    ix->device = dev;
+    ix->dim = cfg->dim;
+    ix->ld = (uint32_t)round_up(cfg->dim, kLdAlign);
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ix;
+        return set_error(BSR_E_HIP, "hipStreamCreate failed");
+    }
+    if (cfg->flags & BSR_FLAG_PROFILE) {
+        for (Events* e : {&ix->ev_emit, &ix->ev_sample, &ix->ev_select, &ix->ev_rescore, &ix->ev_scan, &ix->ev_total}) {
+            int r = e->create();
+            if (r != BSR_OK) { delete ix; return r; }
+        }
+    }
+    *out = ix;
+    return BSR_OK;
+}
+
+void bsr_index_destroy_impl(bsr_index* ix) {
+    if (!ix) return;
+    (void)hipSetDevice(ix->device);
+    (void)hipStreamSynchronize(ix->stream);
+    (void)hipStreamDestroy(ix->stream);
+    delete ix;
+}
+
+int bsr_index_load_impl(bsr_index* ix, const void* rows, uint64_t n_rows, uint64_t global_offset) {
+    if (!ix) return set_error(BSR_E_INVALID, "null index");
+    if (n_rows && !rows) return set_error(BSR_E_INVALID, "null rows");
+    if (n_rows >= (1ull << 31)) return set_error(BSR_E_INVALID, "shard too large (the reference slices with i32 offsets)");
+    BSR_HIP(hipSetDevice(ix->device));
+    ix->loaded = false;
+    ix->n = n_rows;
+    ix->n_pad = round_up(n_rows ? n_rows : 1, kRowPad);
+    ix->global_offset = global_offset;
+    BSR_TRY(ix->rows.ensure(ix->n_pad * (size_t)ix->ld * sizeof(float)));
+    BSR_HIP(hipMemsetAsync(ix->rows.p, 0, ix->n_pad * (size_t)ix->ld * sizeof(float), ix->stream));
+    if (n_rows) BSR_TRY(index_prepare_rows(ix, rows, n_rows, 0));
+    return index_finish_load(ix);
+}
+
+int bsr_index_append_impl(bsr_index* ix, const void* rows, uint64_t n_rows) {
+    if (!ix) return set_error(BSR_E_INVALID, "null index");
+    if (!n_rows) return BSR_OK;
+    if (!rows) return set_error(BSR_E_INVALID, "null rows");
+    BSR_HIP(hipSetDevice(ix->device));
+    const uint64_t old_n = ix->loaded ? ix->n : 0;
+    const uint64_t new_n = old_n + n_rows;
+    if (new_n >= (1ull << 31)) return set_error(BSR_E_INVALID, "shard too large");
+    const uint64_t new_pad = round_up(new_n, kRowPad);
+    if (new_pad * (size_t)ix->ld * sizeof(float) > ix->rows.bytes) {
+        DevBuf grown;
+        BSR_TRY(grown.ensure(new_pad * (size_t)ix->ld * sizeof(float)));
+        BSR_HIP(hipMemsetAsync(grown.p, 0, new_pad * (size_t)ix->ld * sizeof(float), ix->stream));
+        if (old_n)
+            BSR_HIP(hipMemcpyAsync(grown.p, ix->rows.p, old_n * (size_t)ix->ld * sizeof(float),
+                                   hipMemcpyDeviceToDevice, ix->stream));
+        BSR_HIP(hipStreamSynchronize(ix->stream));
+        std::swap(ix->rows.p, grown.p);
+        std::swap(ix->rows.bytes, grown.bytes);
+    }
+    ix->n = new_n;
+    ix->n_pad = new_pad;
+    BSR_TRY(index_prepare_rows(ix, rows, n_rows, old_n));
+    return index_finish_load(ix);
+}
+
+int bsr_index_get_many_impl(const bsr_index* ix, uint64_t offset, uint64_t count, float* out) {
+    if (!ix || (!out && count)) return set_error(BSR_E_INVALID, "null argument");
+    if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
+    if (offset > ix->n || count > ix->n - offset) return set_error(BSR_E_INVALID, "slice out of range");
+    if (!count) return BSR_OK;
+    BSR_HIP(hipSetDevice(ix->device));
+    const hipMemcpyKind kind = is_device_ptr(out) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    BSR_HIP(hipMemcpy2DAsync(out, ix->dim * sizeof(float), ix->rows.as<float>() + offset * ix->ld,
+                             ix->ld * sizeof(float), ix->dim * sizeof(float), count, kind, ix->stream));
+    BSR_HIP(hipStreamSynchronize(ix->stream));
+    return BSR_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// search
+// ---------------------------------------------------------------------------------------
+static int run_exact_scan(bsr_index* ix, const std::vector<int32_t>& ids, uint32_t k) {
+    if (ids.empty()) return BSR_OK;
+    const uint32_t groups = (uint32_t)((ids.size() + kScanQF - 1) / kScanQF);
+    std::vector<int32_t> padded((size_t)groups * kScanQF);
+    for (uint32_t g = 0; g < groups; ++g)
+        for (uint32_t j = 0; j < kScanQF; ++j) {
+            const size_t i = (size_t)g * kScanQF + j;
+            padded[i] = i < ids.size() ? ids[i] : ids[(size_t)g * kScanQF];
+        }
+    BSR_TRY(ix->qids.ensure(padded.size() * sizeof(int32_t)));
+    BSR_HIP(hipMemcpyAsync(ix->qids.p, padded.data(), padded.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           ix->stream));
+    const uint32_t grid = scan_grid_for(ix->n);
+    BSR_TRY(ix->part.ensure((size_t)grid * kScanQF * k * sizeof(uint64_t)));
+    ev_begin(ix, ix->ev_scan);
+    for (uint32_t g = 0; g < groups; ++g) {
+        const uint32_t nqf = (uint32_t)std::min<size_t>(kScanQF, ids.size() - (size_t)g * kScanQF);
+        const int32_t* qid = ix->qids.as<int32_t>() + (size_t)g * kScanQF;
+        BSR_HIP(launch_scan_exact(ix->rows.as<float>(), ix->ld, ix->dim, ix->n, ix->na.as<float>(),
+                                  ix->qf32.as<float>(), qid, nqf, ix->nb.as<float>(), k, grid,
+                                  ix->part.as<uint64_t>(), ix->stream));
+        BSR_HIP(launch_merge_parts(ix->part.as<uint64_t>(), grid, qid, nqf, k, ix->keys.as<uint64_t>(), ix->stream));
+    }
+    ev_end(ix, ix->ev_scan);
+    return BSR_OK;
+}
+
+int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
+    bsr_index* ix = this;
+    if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
+    if (k == 0 || k > ix->cfg.max_k) return set_error(BSR_E_INVALID, "k=%u outside [1, max_k=%u]", k, ix->cfg.max_k);
+    BSR_HIP(hipSetDevice(ix->device));
+    stats = bsr_search_stats{};
+    stats.n_queries = nq;
+    BSR_TRY(o_idx.ensure((size_t)std::max(nq, 1u) * k * sizeof(uint64_t)));
+    BSR_TRY(o_dist.ensure((size_t)std::max(nq, 1u) * k * sizeof(float)));
+    BSR_TRY(o_cnt.ensure((size_t)std::max(nq, 1u) * sizeof(uint32_t)));
+    if (nq == 0) return BSR_OK;
+    if (!queries) return set_error(BSR_E_INVALID, "null queries");
+
+    const uint32_t qpad = (uint32_t)round_up(nq, kGemmBN);
+    BSR_TRY(qf32.ensure((size_t)qpad * ld * sizeof(float)));
+    BSR_TRY(nb.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(qbf.ensure((size_t)qpad * ld * 2));
+    BSR_TRY(qflags.ensure((size_t)qpad * sizeof(uint32_t)));
+    BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
+
+    ev_begin(ix, ev_total);
+    const float* qsrc = queries;
+    if (!is_device_ptr(queries)) {
+        BSR_TRY(q_in.ensure((size_t)nq * dim * sizeof(float)));
+        BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
+        qsrc = q_in.as<float>();
+    }
+    BSR_HIP(launch_query_prep(qsrc, nq, qpad, dim, ld, qf32.as<float>(), nb.as<float>(), qbf.as<uint16_t>(),
+                              qflags.as<uint32_t>(), stream));
+    h_qflags.resize(nq);
+    BSR_HIP(hipMemcpyAsync(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    BSR_HIP(hipStreamSynchronize(stream));
+    std::vector<int32_t> exact_ids;
+    uint32_t n_eligible = 0;
+    for (uint32_t q = 0; q < nq; ++q) {
+        if (h_qflags[q] & kQueryNonFinite)
+            return set_error(BSR_E_NONFINITE, "query %u contains NaN/Inf (the reference panics)", q);
+        if (!(h_qflags[q] & kQueryNoApprox)) ++n_eligible;
+    }
+
+    if (n == 0) {
+        // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
+        BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
+    } else {
+        const bool use_filter = approx_ok && k <= kMaxKForFilter && n_eligible >= kMinBatchForFilter;
+        if (!use_filter) {
+            for (uint32_t q = 0; q < nq; ++q) exact_ids.push_back((int32_t)q);
+            stats.n_exact_direct = nq;
+            BSR_TRY(run_exact_scan(ix, exact_ids, k));
+        } else {
+            const uint32_t kp = 64u * ((k + 54u + 63u) / 64u) - 1u;  // k' candidates, (k'+1) % 64 == 0
+            const uint32_t cap = 16u * (kp + 1u);
+            const uint32_t ks = (kp + 1u) / 8u;
+            stats.n_candidates = kp;
+            BSR_TRY(tau.ensure((size_t)qpad * sizeof(float)));
+            BSR_TRY(cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
+            BSR_TRY(cnt.ensure((size_t)qpad * sizeof(uint32_t)));
+            BSR_TRY(cand_rows.ensure((size_t)nq * kp * sizeof(uint32_t)));
+            BSR_TRY(ncand.ensure((size_t)nq * sizeof(uint32_t)));
+            BSR_TRY(tau_excl.ensure((size_t)nq * sizeof(float)));
+            BSR_TRY(fail.ensure((size_t)(nq + 1) * sizeof(uint32_t)));
+
+            GemmArgs g{};
+            g.A = cbf.as<uint16_t>();
+            g.B = qbf.as<uint16_t>();
+            g.ld = ld;
+            g.n_qt = qpad / kGemmBN;
+
+            uint32_t n_s = 0;
+            if (n > cap) {
+                n_s = (uint32_t)((n + kSampleStride - 1) / kSampleStride);
+                const uint32_t n_rt_s = (n_s + kGemmBM - 1) / kGemmBM;
+                const uint32_t s_ld = n_rt_s * kGemmBM;
+                BSR_TRY(S.ensure((size_t)qpad * s_ld * sizeof(float)));
+                g.a_row_stride = (uint64_t)ld * kSampleStride;
+                g.n_rows = n_s;
+                g.n_rt = n_rt_s;
+                g.S = S.as<float>();
+                g.s_ld = s_ld;
+                ev_begin(ix, ev_sample);
+                BSR_HIP(launch_gemm_sample(g, stream));
+                ev_end(ix, ev_sample);
+                BSR_HIP(launch_select_tau(S.as<float>(), s_ld, n_s, nq, qpad, qflags.as<uint32_t>(), ks,
+                                          tau.as<float>(), stream));
+            } else {
+                BSR_HIP(launch_select_tau(nullptr, 0, 0, nq, qpad, qflags.as<uint32_t>(), ks, tau.as<float>(),
+                                          stream));
+            }
+            BSR_HIP(hipMemsetAsync(cnt.p, 0, (size_t)qpad * sizeof(uint32_t), stream));
+            BSR_HIP(hipMemsetAsync(fail.p, 0, sizeof(uint32_t), stream));
+            g.a_row_stride = ld;
+            g.n_rows = (uint32_t)n;
+            g.n_rt = (uint32_t)((n + kGemmBM - 1) / kGemmBM);
+            g.tau = tau.as<float>();
+            g.cand = cand.as<uint64_t>();
+            g.cnt = cnt.as<uint32_t>();
+            g.cap = cap;
+            ev_begin(ix, ev_emit);
+            BSR_HIP(launch_gemm_emit(g, stream));
+            ev_end(ix, ev_emit);
+            ev_begin(ix, ev_select);
+            BSR_HIP(launch_select_cand(cand.as<uint64_t>(), cnt.as<uint32_t>(), cap, nq, tau.as<float>(), kp,
+                                       cand_rows.as<uint32_t>(), ncand.as<uint32_t>(), tau_excl.as<float>(), stream));
+            ev_end(ix, ev_select);
+            ev_begin(ix, ev_rescore);
+            BSR_HIP(launch_rescore(rows.as<float>(), ld, dim, na.as<float>(), qf32.as<float>(), nb.as<float>(), nq,
+                                   cand_rows.as<uint32_t>(), ncand.as<uint32_t>(), kp, tau_excl.as<float>(), k,
+                                   kEBound, keys.as<uint64_t>(), fail.as<uint32_t>(), fail.as<uint32_t>() + 1,
+                                   stream));
+            ev_end(ix, ev_rescore);
+            uint32_t nfail = 0;
+            BSR_HIP(hipMemcpyAsync(&nfail, fail.p, sizeof nfail, hipMemcpyDeviceToHost, stream));
+            BSR_HIP(hipStreamSynchronize(stream));
+            if (profiling(ix)) {
+                // emitted-candidate count for diagnostics (cheap: qpad counters)
+                std::vector<uint32_t> c(nq);
+                BSR_HIP(hipMemcpy(c.data(), cnt.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
+                for (uint32_t v : c) stats.n_emitted += v;
+            }
+            if (nfail) {
+                h_fail.resize(nfail);
+                BSR_HIP(hipMemcpy(h_fail.data(), fail.as<uint32_t>() + 1, (size_t)nfail * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost));
+                std::sort(h_fail.begin(), h_fail.end());
+                for (uint32_t q : h_fail) exact_ids.push_back((int32_t)q);
+                for (uint32_t q : h_fail)
+                    if (!(h_qflags[q] & kQueryNoApprox)) ++stats.n_fallback;
+                stats.n_exact_direct = nfail - stats.n_fallback;
+                BSR_TRY(run_exact_scan(ix, exact_ids, k));
+            }
+        }
+    }
+    BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, o_idx.as<uint64_t>(), o_dist.as<float>(),
+                            o_cnt.as<uint32_t>(), stream));
+    ev_end(ix, ev_total);
+    return BSR_OK;
+}
+
+static int copy_out(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
+    const size_t nk = (size_t)nq * k;
+    if (out_idx)
+        BSR_HIP(hipMemcpyAsync(out_idx, ix->o_idx.p, nk * sizeof(uint64_t), hipMemcpyDefault, ix->stream));
+    if (out_dist)
+        BSR_HIP(hipMemcpyAsync(out_dist, ix->o_dist.p, nk * sizeof(float), hipMemcpyDefault, ix->stream));
+    if (out_count)
+        BSR_HIP(hipMemcpyAsync(out_count, ix->o_cnt.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, ix->stream));
+    BSR_HIP(hipStreamSynchronize(ix->stream));
+    return BSR_OK;
+}
+
+static void collect_profile(bsr_index* ix) {
+    if (!profiling(ix)) return;
+    bsr_profile& p = ix->prof;
+    ev_collect(ix->ev_emit, p.gemm_emit_ms, p.gemm_emit_launches, 1);
+    ev_collect(ix->ev_sample, p.gemm_sample_ms, p.gemm_sample_launches, 1);
+    ev_collect(ix->ev_select, p.select_ms, p.select_launches, 1);
+    ev_collect(ix->ev_rescore, p.rescore_ms, p.rescore_launches, 1);
+    ev_collect(ix->ev_scan, p.scan_ms, p.scan_launches, 1);
+    ev_collect(ix->ev_total, p.search_ms, p.searches, 1);
+}
+
+int bsr_local_top_k_impl(bsr_index* ix, const float* queries, uint32_t nq, uint32_t k, uint64_t* out_idx,
+                         float* out_dist, uint32_t* out_count) {
+    if (!ix) return set_error(BSR_E_INVALID, "null index");
+    if (nq && (!out_idx || !out_dist || !out_count)) return set_error(BSR_E_INVALID, "null output");
+    BSR_TRY(ix->search_device(queries, nq, k));
+    BSR_TRY(copy_out(ix, nq, k, out_idx, out_dist, out_count));
+    collect_profile(ix);
+    return BSR_OK;
+}
+
+int bsr_index_collect_profile_impl(bsr_index* ix) {
+    collect_profile(ix);
+    return BSR_OK;
+}

@@ -1,0 +1,82 @@
+// internal.hpp -- host-side state shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "bsr.h"
+
+namespace bsr {
+
+int set_error(int code, const char* fmt, ...);
+void clear_error();
+
+#define BSR_HIP(call)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return ::bsr::set_error(BSR_E_HIP, "%s failed: %s (%s:%d)", #call,              \
+                                    hipGetErrorString(e_), __FILE__, __LINE__);             \
+    } while (0)
+
+#define BSR_TRY(call)               \
+    do {                            \
+        int r_ = (call);            \
+        if (r_ != BSR_OK) return r_; \
+    } while (0)
+
+// Growable device allocation (never shrinks).
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need);
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    ~DevBuf() { release(); }
+};
+
+bool is_device_ptr(const void* p);
+int select_device(int device);
+
+static inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+struct Events {
+    hipEvent_t a = nullptr, b = nullptr;
+    bool armed = false;
+    ~Events();
+    int create();
+};
+
+}  // namespace bsr
+
+struct bsr_index {
+    bsr_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t dim = 0, ld = 0;
+    uint64_t n = 0, n_pad = 0, global_offset = 0;
+    bool loaded = false;
+    bool approx_ok = false;
+    uint32_t row_flags = 0;
+
+    bsr::DevBuf rows;  // f32 [n_pad][ld], zero padded: the reference's values
+    bsr::DevBuf na;    // f32 [n_pad]: exact magnitudes (src/metrics.rs:154)
+    bsr::DevBuf cbf;   // bf16 [n_pad][ld]: normalised rows for the MFMA filter
+    bsr::DevBuf flags; // u32
+
+    // per-search scratch
+    bsr::DevBuf q_in, qf32, nb, qbf, qflags, tau, S, cand, cnt, cand_rows, ncand, tau_excl, keys,
+        fail, part, qids, o_idx, o_dist, o_cnt, tmp;
+    std::vector<uint32_t> h_qflags, h_fail;
+
+    bsr_search_stats stats{};
+    bsr_profile prof{};
+    bsr::Events ev_emit, ev_sample, ev_select, ev_rescore, ev_scan, ev_total;
+
+    // Run the local search; results stay in o_idx / o_dist / o_cnt (device, [nq][k]).
+    int search_device(const float* queries, uint32_t nq, uint32_t k);
+};

@@ -1,0 +1,175 @@
+/*
+ * bsr.h -- C ABI of the MI355X-native search engine for the better-search-rag-rust hot path:
+ * block-distributed exact cosine-distance scan + global top-k reduction.
+ *
+ * One process per GPU (the reference's one process per MPI rank).  Every entry point
+ * returns 0 (BSR_OK) or a negative bsr_status; bsr_last_error() gives a thread-local
+ * message.  No C++ exception or panic crosses this boundary.  Plain pointers only: query,
+ * row and output pointers may be host or device (hipMalloc) memory, detected per call.
+ *
+ * Each entry point names the reference item it replaces (paths relative to the reference
+ * repository nichmorgan/better-search-rag-rust):
+ *   bsr_cosine_distance               src/metrics.rs:143-165 (cosine_distance)
+ *   bsr_interval_by_rank              src/mpi_helpers/load_balance.rs:24-42 (interval_by_rank)
+ *   bsr_index_*                       src/vectorstore/polars.rs:79-91,121-169,243-246
+ *                                     (PolarsVectorstore::new/get_many/get/get_count: the
+ *                                     rank's corpus slab, resident in HBM)
+ *   bsr_local_top_k                   src/mpi_helpers/metrics.rs:16-53 (compute_local_top_k)
+ *   bsr_gather_top_k                  src/mpi_helpers/metrics.rs:56-138 (gather_top_k_results)
+ *   bsr_global_top_k                  src/mpi_helpers/metrics.rs:141-171 (compute_global_top_k)
+ *   bsr_parallel_top_k_similarity_search
+ *                                     src/mpi_helpers/metrics.rs:174-206
+ *                                     (parallel_top_k_similarity_search)
+ *
+ * Results are bit-identical to the reference's: indices in (distance asc, index asc)
+ * order, each distance the exact f32 the reference computes (sequential f32 sums, no FMA,
+ * correctly rounded sqrt/div, identical-vector shortcut).  Deviations (documented in
+ * DESIGN.md): non-finite inputs return BSR_E_NONFINITE where the reference panics; a query
+ * whose length differs from the index dimension returns BSR_E_DIM where the reference
+ * scores every row 1.0.
+ */
+#ifndef BSR_H
+#define BSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    BSR_OK = 0,
+    BSR_E_INVALID = -1,   /* bad argument / null pointer / k out of range */
+    BSR_E_NONFINITE = -2, /* NaN or Inf in a query or row (the reference panics) */
+    BSR_E_HIP = -3,       /* HIP runtime error (message in bsr_last_error) */
+    BSR_E_NOMEM = -4,     /* device allocation failed */
+    BSR_E_RCCL = -5,      /* RCCL error */
+    BSR_E_DIM = -6,       /* query length != index dimension */
+    BSR_E_STATE = -7,     /* call out of order (e.g. search before load) */
+    BSR_E_NODEVICE = -8   /* no HIP device visible: the engine has no CPU fallback */
+} bsr_status;
+
+typedef enum { BSR_F32 = 0, BSR_BF16 = 1 } bsr_dtype;
+
+typedef struct {
+    uint32_t dim;    /* embedding length (768 in the reference, src/main.rs:117) */
+    uint32_t dtype;  /* bsr_dtype of the stored rows */
+    uint32_t max_k;  /* largest top_k a search may ask for (<= BSR_MAX_K) */
+    uint32_t flags;  /* BSR_FLAG_* */
+    int32_t device;  /* HIP device ordinal; -1 = current device */
+} bsr_config;
+
+#define BSR_MAX_K 256u
+#define BSR_FLAG_EXACT_ONLY 1u /* never use the MFMA candidate stage (always full exact scan) */
+#define BSR_FLAG_PROFILE 2u    /* record per-kernel HIP events (bsr_index_profile) */
+
+/* Mirrors RankInterval {start_index, end_index} (load_balance.rs:8-17). end < start means
+ * an empty block, as in the reference's release build. */
+typedef struct {
+    uint64_t start_index;
+    uint64_t end_index;
+} bsr_rank_interval;
+
+typedef struct bsr_index bsr_index; /* one rank's corpus shard, resident in HBM */
+typedef struct bsr_comm bsr_comm;   /* RCCL communicator over the ranks (one GPU each) */
+
+/* Per-search statistics of the last bsr_local_top_k on an index. */
+typedef struct {
+    uint32_t n_queries;
+    uint32_t n_exact_direct;   /* queries answered by the full exact scan by design */
+    uint32_t n_fallback;       /* queries whose MFMA candidate set failed certification */
+    uint32_t n_candidates;     /* k' candidates rescored per query */
+    uint64_t n_emitted;        /* candidates emitted by the MFMA filter (all queries) */
+} bsr_search_stats;
+
+/* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts
+ * since the last reset, measured with hipEvents on the index's stream. */
+typedef struct {
+    double gemm_emit_ms;  uint64_t gemm_emit_launches;  /* dominant kernel */
+    double gemm_sample_ms; uint64_t gemm_sample_launches;
+    double select_ms;     uint64_t select_launches;
+    double rescore_ms;    uint64_t rescore_launches;
+    double scan_ms;       uint64_t scan_launches;
+    double search_ms;     uint64_t searches;             /* whole bsr_local_top_k */
+} bsr_profile;
+
+/* ---- errors / device -------------------------------------------------------------- */
+const char* bsr_last_error(void);
+const char* bsr_status_string(int status);
+int bsr_device_count(int* out_count);
+const char* bsr_version(void);
+
+/* ---- a-1: src/metrics.rs:143-165, one pair, computed on the GPU ------------------ */
+int bsr_cosine_distance(const float* a, uint32_t len_a, const float* b, uint32_t len_b,
+                        float* out);
+
+/* ---- a-3: src/mpi_helpers/load_balance.rs:24-42 ---------------------------------- */
+int bsr_interval_by_rank(int32_t rank, int32_t size, uint64_t count, bsr_rank_interval* out);
+
+/* ---- the rank's shard (read side of src/vectorstore/polars.rs) ------------------- */
+int bsr_index_create(const bsr_config* cfg, bsr_index** out);
+void bsr_index_destroy(bsr_index* ix);
+/* Copy n_rows row-major rows (f32, or bf16 bits when cfg.dtype == BSR_BF16) into HBM and
+ * precompute per-row state.  global_offset is the global index of local row 0
+ * (interval_by_rank(rank,size,N).start_index).  Replaces any previous contents. */
+int bsr_index_load(bsr_index* ix, const void* rows, uint64_t n_rows, uint64_t global_offset);
+/* Append rows after the current ones (PolarsVectorstore::append_many, polars.rs:101-119). */
+int bsr_index_append(bsr_index* ix, const void* rows, uint64_t n_rows);
+int bsr_index_count(const bsr_index* ix, uint64_t* out);                /* get_count */
+int bsr_index_global_offset(const bsr_index* ix, uint64_t* out);
+/* Copy `count` rows starting at local row `offset` into out (f32, host or device):
+ * PolarsVectorstore::get_many(SliceArgs{offset,length}) / get (polars.rs:121-169). */
+int bsr_index_get_many(const bsr_index* ix, uint64_t offset, uint64_t count, float* out);
+
+/* ---- a-2: compute_local_top_k for n_queries queries (row-major [n_queries][dim] f32).
+ * out_idx/out_dist are [n_queries][k]; row q holds out_count[q] = min(k, n_rows) entries
+ * in (distance asc, global index asc) order.  Indices are global (offset added). ------ */
+int bsr_local_top_k(bsr_index* ix, const float* queries, uint32_t n_queries, uint32_t k,
+                    uint64_t* out_idx, float* out_dist, uint32_t* out_count);
+
+/* ---- a-5: compute_global_top_k over n_lists per-rank lists, for n_queries queries.
+ * Input list l of query q: idx[(l*n_queries+q)*k_in ..] with count[l*n_queries+q]
+ * entries.  Rank-order concatenation + stable sort by distance + dedupe, keep k.
+ * Host memory only (the reference merges on rank 0's host). ------------------------- */
+int bsr_global_top_k(const uint64_t* idx, const float* dist, const uint32_t* count,
+                     uint32_t n_lists, uint32_t n_queries, uint32_t k_in, uint32_t k,
+                     uint64_t* out_idx, float* out_dist, uint32_t* out_count);
+
+/* ---- communicator (replaces the MPI world; RCCL over xGMI) ----------------------- */
+#define BSR_UNIQUE_ID_BYTES 128
+int bsr_comm_unique_id(uint8_t out_id[BSR_UNIQUE_ID_BYTES]); /* on rank 0; broadcast it */
+int bsr_comm_init(const uint8_t id[BSR_UNIQUE_ID_BYTES], int32_t rank, int32_t size,
+                  int32_t device, bsr_comm** out);
+void bsr_comm_destroy(bsr_comm* comm);
+int bsr_comm_rank(const bsr_comm* comm, int32_t* rank, int32_t* size);
+
+/* ---- a-4: gather_top_k_results.  Every rank passes its [n_queries][k] local lists;
+ * the root (rank 0) receives [size][n_queries][k] lists + counts in rank order
+ * (host buffers, may be NULL on non-root ranks).  Collective: every rank calls it. ---- */
+int bsr_gather_top_k(bsr_comm* comm, const uint64_t* local_idx, const float* local_dist,
+                     const uint32_t* local_count, uint32_t n_queries, uint32_t k,
+                     uint64_t* root_idx, float* root_dist, uint32_t* root_count);
+
+/* ---- a-6: parallel_top_k_similarity_search: local search on this rank's shard,
+ * RCCL all-gather of the partial lists, host merge.  Root gets the global top-k in
+ * out_*; other ranks get out_count[q] = 0 (the reference's None).  comm may be NULL for
+ * a single-rank run. ----------------------------------------------------------------- */
+int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries,
+                                         uint32_t n_queries, uint32_t k, uint64_t* out_idx,
+                                         float* out_dist, uint32_t* out_count);
+
+/* ---- diagnostics ------------------------------------------------------------------ */
+int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out);
+int bsr_index_profile(bsr_index* ix, bsr_profile* out, int reset);
+
+/* ---- synthetic data (bench / tests): U(-1,1) f32 from a counter-based hash of
+ * (seed, global element index), written on the device: value(row, col) for rows
+ * [row0, row0+n_rows).  Identical on every rank and GPU. --------------------------- */
+int bsr_synth_uniform(float* dev_out, uint64_t row0, uint64_t n_rows, uint32_t dim,
+                      uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSR_H */

@@ -1,0 +1,281 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit for bit.
+
+Indices, their order and the f32 distance bits must equal the reference restatement's
+(north_star: indices/ranks bit-exact, distances within 1e-5 -- we require
+exact bits, the stronger bar).  Sizes keep the oracle to seconds."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(got, want, ctx=""):
+    gi, gd, gc = got
+    wi, wd, wc = want
+    assert np.array_equal(gc, wc), (ctx, gc, wc)
+    for q in range(len(wc)):
+        c = int(wc[q])
+        assert np.array_equal(gi[q, :c], wi[q, :c]), (ctx, q, gi[q, :c], wi[q, :c])
+        assert np.array_equal(gd[q, :c].view(np.uint32), wd[q, :c].view(np.uint32)), (ctx, q)
+
+
+def _index(bsr_mod, rows, max_k=256, flags=0, offset=0):
+    ix = bsr_mod.Index(rows.shape[1], max_k=max_k, device=0, flags=flags)
+    ix.load(rows, offset)
+    return ix
+
+
+# ---- a-1 ---------------------------------------------------------------------------------
+def test_cosine_known_answers_on_gpu(bsr_mod, gpu):
+    with open(os.path.join(GOLDEN, "known_answers.json")) as f:
+        ka = json.load(f)
+    for c in ka["cosine_distance"]:
+        got = bsr_mod.cosine_distance(np.array(c["a"], np.float32), np.array(c["b"], np.float32))
+        assert np.float32(got).view(np.uint32) == c["expected_bits"], c["name"]
+
+
+def test_cosine_random_pairs_bitexact(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(0)
+    for i in range(60):
+        d = int(rng.choice([1, 2, 3, 17, 768, 1024]))
+        a = (rng.uniform(-1, 1, d) * 10.0 ** rng.integers(-20, 20)).astype(np.float32)
+        b = (rng.uniform(-1, 1, d) * 10.0 ** rng.integers(-20, 20)).astype(np.float32)
+        if i % 7 == 0:
+            b = a.copy()
+        if i % 11 == 0:
+            b = a + np.float32(3e-11)
+        want = oracle_mod.cosine_distance(a, b)
+        got = bsr_mod.cosine_distance(a, b)
+        assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32), (i, got, want)
+
+
+# ---- golden fixtures ------------------------------------------------------------------
+@pytest.mark.parametrize("exact_only", [False, True])
+def test_golden_search(bsr_mod, gpu, exact_only):
+    from golden.make_golden import corpus_case
+    g = np.load(os.path.join(GOLDEN, "search_golden.npz"))
+    for ci in range(int(g["n_cases"])):
+        seed, n, dim, nq, k, P = (int(x) for x in g[f"c{ci}_spec"])
+        rows = corpus_case(seed, n, dim) if n > 20 else bsr_mod.synth_uniform_np(0, n, dim, seed)
+        q = bsr_mod.synth_uniform_np(0, nq, dim, seed + 1000)
+        if n > 20:
+            q[0] = rows[5]
+        if nq > 1:
+            q[1] = rows[min(3, n - 1)]
+        ix = _index(bsr_mod, rows, flags=1 if exact_only else 0)
+        # repeat the queries so the batched MFMA filter path (>= 16 queries) runs too
+        reps = 1 if exact_only else 8
+        qq = np.concatenate([q] * reps)
+        gi, gd, gc = ix.local_top_k(qq, k)
+        want = (g[f"c{ci}_idx"], g[f"c{ci}_dist_bits"].view(np.float32), g[f"c{ci}_count"])
+        for r in range(reps):
+            sl = slice(r * nq, (r + 1) * nq)
+            _assert_same((gi[sl], gd[sl], gc[sl]), want, f"case {ci} rep {r}")
+
+
+# ---- exact scan (small batches) and filter path (batches) vs the oracle --------------
+@pytest.mark.parametrize("n,dim,nq,k", [
+    (1, 768, 1, 10), (5, 768, 3, 10), (257, 768, 2, 1), (1000, 768, 5, 64), (3000, 130, 9, 100),
+    (4097, 768, 4, 256), (20000, 768, 8, 50)])
+def test_exact_scan_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
+    rng = np.random.default_rng(n + dim + k)
+    rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
+    if n > 10:
+        rows[n // 2] = rows[1]
+        rows[3] = 0
+    qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
+    qs[0] = rows[min(1, n - 1)]
+    ix = _index(bsr_mod, rows)
+    got = ix.local_top_k(qs, k)
+    assert ix.last_stats().n_exact_direct == nq
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
+
+
+@pytest.mark.parametrize("n,dim,nq,k", [
+    (20000, 768, 32, 10),   # config 1 stand-in (JabRef ~20k chunks, 32 queries, top-10)
+    (20000, 768, 40, 50),   # the reference's own k = 50 (src/main.rs:110)
+    (30000, 256, 20, 100),
+    (2500, 768, 64, 10),    # n <= candidate cap: no sample pass, tau = -inf
+    (50000, 96, 17, 200),
+])
+def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
+    rng = np.random.default_rng(7 * n + k)
+    rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
+    rows[n - 1] = rows[0]            # duplicate pair far apart
+    rows[10] = 0                     # zero row
+    rows[12] = rows[20] * np.float32(3.0)
+    qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
+    qs[0] = rows[0]
+    qs[1] = rows[20]
+    ix = _index(bsr_mod, rows)
+    got = ix.local_top_k(qs, k)
+    st = ix.last_stats()
+    assert st.n_exact_direct == 0 and st.n_candidates >= k
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
+    # both copies of row 0 lead query 0's list at distance 0, smaller index first
+    assert list(got[0][0, :2]) == [0, n - 1] and got[1][0, 0] == 0 and got[1][0, 1] == 0
+
+
+def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu):
+    # Clustered embeddings (dense neighbourhoods) stress the certification; any query it
+    # cannot certify must fall back to the exact scan and still be exact.
+    rng = np.random.default_rng(42)
+    centers = rng.normal(size=(20, 768)).astype(np.float32)
+    rows = (centers[rng.integers(0, 20, 40000)] + 0.05 * rng.normal(size=(40000, 768))).astype(np.float32)
+    qs = (centers[rng.integers(0, 20, 24)] + 0.05 * rng.normal(size=(24, 768))).astype(np.float32)
+    ix = _index(bsr_mod, rows)
+    got = ix.local_top_k(qs, 10)
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "clusters")
+
+
+def test_global_offset_and_get_many(bsr_mod, gpu):
+    rng = np.random.default_rng(1)
+    rows = rng.uniform(-1, 1, (300, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, offset=1000)
+    assert ix.get_count() == 300 and ix.global_offset() == 1000
+    assert np.array_equal(ix.get_many(bsr_mod.SliceArgs(10, 5)), rows[10:15])
+    assert np.array_equal(ix.get(299), rows[299])
+    assert np.array_equal(ix.get_many(), rows)
+    gi, gd, gc = ix.local_top_k(rows[[42]], 3)
+    assert gi[0, 0] == 1042 and gd[0, 0] == 0
+
+
+def test_append_many_then_search(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(2)
+    rows = rng.uniform(-1, 1, (3000, 768)).astype(np.float32)
+    ix = bsr_mod.Index(768, max_k=16, device=0)
+    ix.load(rows[:1000])
+    ix.append_many(rows[1000:2500])
+    ix.append_many(rows[2500:])
+    assert ix.get_count() == 3000
+    qs = rng.uniform(-1, 1, (20, 768)).astype(np.float32)
+    _assert_same(ix.local_top_k(qs, 16), oracle_mod.parallel_top_k(rows, qs, 16), "append")
+
+
+def test_errors(bsr_mod, gpu):
+    ix = bsr_mod.Index(768, max_k=10, device=0)
+    with pytest.raises(bsr_mod.BsrError) as e:
+        ix.local_top_k(np.zeros((1, 768), np.float32), 5)
+    assert e.value.status == -7  # not loaded
+    rows = np.ones((10, 768), np.float32)
+    rows[3, 4] = np.nan
+    with pytest.raises(bsr_mod.BsrError) as e:
+        ix.load(rows)
+    assert e.value.status == -2
+    ix.load(np.ones((10, 768), np.float32))
+    with pytest.raises(bsr_mod.BsrError) as e:
+        ix.local_top_k(np.zeros((1, 768), np.float32), 11)
+    assert e.value.status == -1
+    q = np.zeros((1, 768), np.float32)
+    q[0, 0] = np.inf
+    with pytest.raises(bsr_mod.BsrError) as e:
+        ix.local_top_k(q, 5)
+    assert e.value.status == -2
+    with pytest.raises(bsr_mod.BsrError) as e:
+        ix.local_top_k(np.zeros((1, 700), np.float32), 5)
+    assert e.value.status == -6
+
+
+def test_zero_and_tiny_queries_take_exact_path(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(3)
+    rows = rng.uniform(-1, 1, (5000, 768)).astype(np.float32)
+    rows[17] = 0
+    rows[18] = np.float32(1e-12)  # within 1e-10 of the zero query -> identical -> 0.0
+    qs = rng.uniform(-1, 1, (20, 768)).astype(np.float32)
+    qs[2] = 0
+    qs[3] = np.float32(1e-25)
+    ix = _index(bsr_mod, rows)
+    got = ix.local_top_k(qs, 10)
+    assert ix.last_stats().n_exact_direct >= 2
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "zero query")
+
+
+def test_overflowing_rows_force_exact(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(4)
+    rows = rng.uniform(-1, 1, (3000, 768)).astype(np.float32)
+    rows[5] *= np.float32(1e19)   # |a|^2 overflows -> reference distance 1.0 or 2.0
+    qs = rng.uniform(-1, 1, (20, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows)
+    got = ix.local_top_k(qs, 10)
+    assert ix.last_stats().n_exact_direct == 20
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "overflow")
+
+
+def test_bf16_corpus_widened(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(5)
+    f = rng.uniform(-1, 1, (4000, 768)).astype(np.float32)
+    bits = (f.view(np.uint32) + 0x7FFF + ((f.view(np.uint32) >> 16) & 1)) >> 16
+    b16 = bits.astype(np.uint16)
+    widened = (b16.astype(np.uint32) << 16).view(np.float32)
+    ix = bsr_mod.Index(768, max_k=100, device=0, dtype=bsr_mod.BSR_BF16)
+    ix.load(b16)
+    qs = widened[:20].copy()
+    _assert_same(ix.local_top_k(qs, 100), oracle_mod.parallel_top_k(widened, qs, 100), "bf16")
+
+
+# ---- sharding: results independent of the number of shards ----------------------------
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_shards_on_one_gpu_merge_to_single(bsr_mod, oracle_mod, gpu, P):
+    rng = np.random.default_rng(P)
+    N = 24001
+    rows = rng.uniform(-1, 1, (N, 768)).astype(np.float32)
+    rows[N - 3] = rows[2]
+    qs = rng.uniform(-1, 1, (32, 768)).astype(np.float32)
+    qs[0] = rows[2]
+    k = 10
+    li = np.zeros((P, 32, k), np.uint64)
+    ld = np.zeros((P, 32, k), np.float32)
+    lc = np.zeros((P, 32), np.uint32)
+    for r in range(P):
+        iv = bsr_mod.interval_by_rank(r, P, N)
+        s, e = iv.start_index, max(iv.start_index, iv.end_index)
+        if s >= N:
+            continue
+        ix = _index(bsr_mod, rows[s:e], max_k=k, offset=s)
+        li[r], ld[r], lc[r] = ix.local_top_k(qs, k)
+    got = bsr_mod.merge_top_k_lists(li, ld, lc, k)
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k, size=P), f"P={P}")
+
+
+def test_parallel_search_single_rank_comm(bsr_mod, oracle_mod, gpu):
+    rng = np.random.default_rng(8)
+    rows = rng.uniform(-1, 1, (10000, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=50)
+    comm = bsr_mod.Comm(bsr_mod.Comm.unique_id(), 0, 1, 0)
+    res = bsr_mod.parallel_top_k_similarity_search(comm, 0, 1, ix, 50, rows[0])
+    wi, wd, wc = oracle_mod.parallel_top_k(rows, rows[[0]], 50)
+    assert [i for i, _ in res] == [int(x) for x in wi[0]]
+    assert np.array_equal(np.array([d for _, d in res], np.float32).view(np.uint32), wd[0].view(np.uint32))
+    assert bsr_mod.calculate_accuracy_metrics(res, 0, 50) == (1.0, 1.0, 1.0)
+    comm.close()
+
+
+def test_synth_uniform_device_matches_host_replica(bsr_mod, gpu):
+    import torch
+    t = torch.empty((37, 768), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(t.data_ptr(), 1000, 37, 768, 42)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), bsr_mod.synth_uniform_np(1000, 37, 768, 42))
+
+
+def test_device_pointer_inputs(bsr_mod, oracle_mod, gpu):
+    import torch
+    rng = np.random.default_rng(9)
+    rows = rng.uniform(-1, 1, (6000, 768)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (33, 768)).astype(np.float32)
+    ix = bsr_mod.Index(768, max_k=10, device=0)
+    ix.load(torch.from_numpy(rows).cuda())
+    torch.cuda.synchronize()
+    dq = torch.from_numpy(qs).cuda()
+    oi = torch.empty((33, 10), dtype=torch.int64, device="cuda:0")
+    od = torch.empty((33, 10), dtype=torch.float32, device="cuda:0")
+    oc = torch.empty(33, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    ix.local_top_k_device(dq, 33, 10, oi, od, oc)
+    got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "device ptrs")
