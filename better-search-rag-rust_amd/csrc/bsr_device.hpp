@@ -82,13 +82,17 @@ struct WaveTopK {
         for (int e = 0; e < E; ++e) v[e] = kKeyNone;
     }
     // Key at (wave-uniform) position pos.
+    // (Each entry is read out as a wave-uniform scalar and selected afterwards: selecting
+    // v[e] first lets LLVM fold the chain into a dynamically indexed stack array.)
     __device__ __forceinline__ uint64_t at(int pos) const {
         const int e = pos >> 6, l = pos & 63;
-        uint64_t x = v[0];
+        uint64_t x = readlane64(v[0], l);
 #pragma unroll
-        for (int i = 1; i < E; ++i)
-            if (i == e) x = v[i];
-        return readlane64(x, l);
+        for (int i = 1; i < E; ++i) {
+            const uint64_t y = readlane64(v[i], l);
+            x = (i == e) ? y : x;
+        }
+        return x;
     }
     // Insert a wave-uniform key (duplicates allowed; the largest entry falls off).
     __device__ __forceinline__ void insert(uint64_t x) {

@@ -298,7 +298,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     if (nq == 0) return BSR_OK;
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
 
-    const uint32_t qpad = (uint32_t)round_up(nq, kGemmBN);
+    const uint32_t qpad = (uint32_t)round_up(nq, gemm_query_pad());
     BSR_TRY(qf32.ensure((size_t)qpad * ld * sizeof(float)));
     BSR_TRY(nb.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(qbf.ensure((size_t)qpad * ld * 2));
@@ -351,13 +351,14 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
             g.A = cbf.as<uint16_t>();
             g.B = qbf.as<uint16_t>();
             g.ld = ld;
-            g.n_qt = qpad / kGemmBN;
+            g.n_qt = qpad / gemm_query_pad();
+            const uint32_t BM = gemm_row_tile();
 
             uint32_t n_s = 0;
             if (n > cap) {
                 n_s = (uint32_t)((n + kSampleStride - 1) / kSampleStride);
-                const uint32_t n_rt_s = (n_s + kGemmBM - 1) / kGemmBM;
-                const uint32_t s_ld = n_rt_s * kGemmBM;
+                const uint32_t n_rt_s = (n_s + BM - 1) / BM;
+                const uint32_t s_ld = n_rt_s * BM;
                 BSR_TRY(S.ensure((size_t)qpad * s_ld * sizeof(float)));
                 g.a_row_stride = (uint64_t)ld * kSampleStride;
                 g.n_rows = n_s;
@@ -377,7 +378,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
             BSR_HIP(hipMemsetAsync(fail.p, 0, sizeof(uint32_t), stream));
             g.a_row_stride = ld;
             g.n_rows = (uint32_t)n;
-            g.n_rt = (uint32_t)((n + kGemmBM - 1) / kGemmBM);
+            g.n_rt = (uint32_t)((n + BM - 1) / BM);
             g.tau = tau.as<float>();
             g.cand = cand.as<uint64_t>();
             g.cnt = cnt.as<uint32_t>();

@@ -51,6 +51,10 @@ struct GemmArgs {
     uint32_t* cnt;          // emit: [qpad] counters
     uint32_t cap;
 };
+// Tile geometry of the active filter kernel (BSR_GEMM_VARIANT=1 selects the v1 128x128
+// kernel for A/B comparisons; default v2 = persistent 256x256).
+uint32_t gemm_query_pad();
+uint32_t gemm_row_tile();
 hipError_t launch_gemm_sample(const GemmArgs& a, hipStream_t s);
 hipError_t launch_gemm_emit(const GemmArgs& a, hipStream_t s);
 

@@ -1,0 +1,46 @@
+"""Turn rocprofv3 --pmc CSVs of bench.py into profiles/pmc_traffic.json (tooling).
+
+HBM bytes per launch of the dominant kernel = FETCH_SIZE * 1024 * 2 + WRITE_SIZE * 1024:
+on gfx950 FETCH_SIZE (KB) reports half of the bytes of a wide coalesced read
+(MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for 16-B stores.  FETCH_SIZE and
+WRITE_SIZE are collected in separate passes (TCC counter slots).
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <rows> <queries> <out.json>
+"""
+import csv
+import glob
+import json
+import sys
+
+
+def per_kernel(d, counter):
+    vals = {}
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            vals.setdefault(name, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    fdir, wdir, rows, queries, out = sys.argv[1:6]
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    emit = [k for k in fetch if "gemm_filter" in k and "<true" in k]
+    res = {"rows": int(rows), "queries": int(queries), "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k)
+        w = write.get(k)
+        res["kernels"][k] = {"fetch_size_kb": f, "write_size_kb": w,
+                             "hbm_bytes_corrected": (f * 1024 * 2 if f is not None else 0) +
+                                                    (w * 1024 if w is not None else 0)}
+    if emit:
+        res["dominant_kernel"] = emit[0]
+        res["hbm_bytes_per_launch"] = res["kernels"][emit[0]]["hbm_bytes_corrected"]
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}))
+
+
+if __name__ == "__main__":
+    main()
