@@ -24,6 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "better-search-rag-rust_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 PEAK_BF16_DENSE = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
+PEAK_I8_DENSE = 5.0e15     # MI355X dense int8 MFMA: 2x the bf16 rate per clock (same guide)
 PEAK_HBM = 8.0e12          # MI355X HBM3E (spec)
 
 
@@ -40,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle (rank 0, N=1)")
+    ap.add_argument("--filter", choices=["i8", "bf16"], default="i8",
+                    help="MFMA candidate-filter operand type (results are exact either way)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -72,7 +75,8 @@ def main():
     start, n_local = iv.start_index, iv.get_count()
 
     # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index.
-    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE)
+    fflag = bsr.BSR_FLAG_FILTER_BF16 if args.filter == "bf16" else 0
+    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE | fflag)
     shard = torch.empty((max(n_local, 1), D), dtype=torch.float32, device=dev)
     if n_local:
         bsr.synth_uniform(shard.data_ptr(), start, n_local, D, 42)
@@ -146,10 +150,12 @@ def main():
         flops = 2.0 * Q * n_local * D
         achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
         traffic = None
+        peak = PEAK_I8_DENSE if args.filter == "i8" else PEAK_BF16_DENSE
+        kname = f"k_filter<Op{'I8' if args.filter == 'i8' else 'BF16'}, true>"
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
-                if pm.get("rows") == n_local and pm.get("queries") == Q:
+                if pm.get("rows") == n_local and pm.get("queries") == Q and pm.get("filter") == args.filter:
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -165,23 +171,26 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.filter,
             "data": "synthetic U(-1,1) f32 corpus generated on device (seed 42), 1000 queries (seed 43, query 0 = row 0)",
             "config": {
                 "workload": f"configs[1] per GPU: {n_local} x {D} f32 rows per GPU ({n_total} total), "
                             f"{Q} batched queries, top-{K}; value = queries x 1M-row shards / s",
                 "rows_total": n_total, "rows_per_gpu": n_local, "queries": Q, "top_k": K, "dim": D,
                 "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank) + RCCL all-gather",
-                "filter": "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates, exact sequential-f32 rescore",
+                "filter": ("int8 MFMA (v_mfma_i32_32x32x32_i8) candidates" if args.filter == "i8" else
+                           "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates") +
+                          ", exact sequential-f32 rescore of k'=63 per query, certified (DESIGN.md §4)",
                 "qps_over_full_corpus": round(Q / (ms_per_step * 1e-3), 2),
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
             "p50_config": f"1 query over {n_total} rows (exact scan, HBM-bound)",
             "roofline": {
-                "bound": "mfma", "kernel": "k_gemm_filter<emit>",
+                "bound": "mfma", "kernel": kname,
                 "achieved": round(achieved, 2) if achieved else None,
-                "peak": PEAK_BF16_DENSE / 1e12, "unit": "TFLOP/s",
-                "frac": round(achieved * 1e12 / PEAK_BF16_DENSE, 4) if achieved else None,
+                "peak": peak / 1e12, "unit": "TOP/s" if args.filter == "i8" else "TFLOP/s",
+                "frac": round(achieved * 1e12 / peak, 4) if achieved else None,
+                "frac_of_bf16_peak": round(achieved * 1e12 / PEAK_BF16_DENSE, 4) if achieved else None,
                 "traffic": traffic,
                 "algorithmic_flops_per_launch": flops,
                 "avg_launch_ms": round(emit_ms, 5),
@@ -198,6 +207,8 @@ def main():
             "fallback_queries_per_step": stats_fb / args.steps,
             "candidates_per_query": st.n_candidates,
             "self_query_rank1": self_ok,
+            "emitted_per_query": round(st.n_emitted / max(Q, 1), 1),
+            "row_ebound": round(float(st.row_ebound), 6),
         }
         # HBM roofline of the single-query scan kernel (bytes = N*d*4 per query).
         scan_ms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)

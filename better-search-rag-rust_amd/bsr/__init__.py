@@ -34,6 +34,8 @@ BSR_BF16 = 1
 BSR_MAX_K = 256
 BSR_FLAG_EXACT_ONLY = 1
 BSR_FLAG_PROFILE = 2
+BSR_FLAG_FILTER_BF16 = 4
+FILTER_I8, FILTER_BF16 = 0, 1
 ROOT = 0  # src/mpi_helpers/mod.rs:8
 
 
@@ -55,7 +57,8 @@ class _Interval(ctypes.Structure):
 class SearchStats(ctypes.Structure):
     _fields_ = [("n_queries", ctypes.c_uint32), ("n_exact_direct", ctypes.c_uint32),
                 ("n_fallback", ctypes.c_uint32), ("n_candidates", ctypes.c_uint32),
-                ("n_emitted", ctypes.c_uint64)]
+                ("n_emitted", ctypes.c_uint64), ("filter_op", ctypes.c_uint32),
+                ("row_ebound", ctypes.c_float)]
 
 
 class Profile(ctypes.Structure):

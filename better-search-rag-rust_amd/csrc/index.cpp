@@ -1,13 +1,14 @@
 // index.cpp -- the rank's corpus shard in HBM and the local search pipeline
 // (compute_local_top_k, src/mpi_helpers/metrics.rs:16-53, for a batch of queries).
 //
-// Pipeline for a batch:
-//   1. query prep          exact |b|, normalised bf16 copy, flags
-//   2. sample filter       bf16 MFMA scores of every 32nd row -> tau0 = ks-th best (per query)
-//   3. emit filter         bf16 MFMA scores of every row; rows with score >= tau0 -> candidates
-//   4. select              top-(k'+1) candidates by approximate score
-//   5. rescore             exact sequential-f32 distances of k' candidates, top-k, certify
-//   6. fallback            exact full scan for any uncertified / ineligible query
+// Pipeline for a batch, all on the index's stream:
+//   1. query prep     exact |b| (src/metrics.rs:155), flags, the filter operand (int8 + scale,
+//                     or bf16) and the per-query certification bound E_q
+//   2. sample filter  MFMA scores of every 32nd row -> tau0 (per query)
+//   3. emit filter    MFMA scores of every row; rows with score >= tau0 -> candidates
+//   4. select         top-(k'+1) candidates by approximate score
+//   5. rescore        exact sequential-f32 distances of k' candidates, top-k, certify
+//   6. one status readback; fallback: exact full scan of any uncertified / ineligible query
 // Small batches, k > 200, or an index with out-of-range norms use the exact scan only.
 #include <math.h>
 #include <stdio.h>
@@ -20,11 +21,6 @@
 
 namespace bsr {
 
-// Certification bound on |approximate cosine - reference cosine|: two bf16
-// roundings of normalised operands (2u+u^2, u = 2^-8), the f32 accumulation of the MFMA
-// and of the reference (2*gamma_768), f32 magnitudes and the reference's final rounding,
-// with margin.
-constexpr double kEBound = 8.5e-3;
 constexpr uint32_t kMinBatchForFilter = 16;
 constexpr uint32_t kMaxKForFilter = 200;
 
@@ -139,26 +135,34 @@ static int index_prepare_rows(bsr_index* ix, const void* rows, uint64_t n_rows, 
     return BSR_OK;
 }
 
+// Per-row state: the reference's magnitudes, row flags and the filter operand.
 static int index_finish_load(bsr_index* ix) {
     BSR_TRY(ix->na.ensure(ix->n_pad * sizeof(float)));
-    BSR_TRY(ix->cbf.ensure(ix->n_pad * (size_t)ix->ld * 2));
-    BSR_TRY(ix->flags.ensure(sizeof(uint32_t)));
-    BSR_HIP(hipMemsetAsync(ix->flags.p, 0, sizeof(uint32_t), ix->stream));
+    BSR_TRY(ix->fop.ensure((size_t)ix->n_pad * ix->op_row_bytes));
+    BSR_TRY(ix->flags.ensure(2 * sizeof(uint32_t)));
+    BSR_HIP(hipMemsetAsync(ix->flags.p, 0, 2 * sizeof(uint32_t), ix->stream));
     BSR_HIP(hipMemsetAsync(ix->na.p, 0, ix->n_pad * sizeof(float), ix->stream));
     if (ix->n) BSR_HIP(launch_row_norms(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->na.as<float>(),
                                         ix->flags.as<uint32_t>(), ix->stream));
-    BSR_HIP(launch_rows_to_bf16n(ix->rows.as<float>(), ix->na.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld,
-                                 ix->cbf.as<uint16_t>(), ix->stream));
-    uint32_t f = 0;
-    BSR_HIP(hipMemcpyAsync(&f, ix->flags.p, sizeof f, hipMemcpyDeviceToHost, ix->stream));
+    if (ix->op == kFilterBF16) {
+        BSR_HIP(launch_rows_to_bf16n(ix->rows.as<float>(), ix->na.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld,
+                                     ix->fop.as<uint16_t>(), ix->stream));
+    } else {
+        BSR_TRY(ix->ascale.ensure(ix->n_pad / kQuantBlock * sizeof(float)));
+        BSR_HIP(launch_rows_to_i8(ix->rows.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld, ix->fop.as<int8_t>(),
+                                  ix->ascale.as<float>(), ix->flags.as<uint32_t>() + 1, ix->stream));
+    }
+    uint32_t f[2] = {0, 0};
+    BSR_HIP(hipMemcpyAsync(f, ix->flags.p, sizeof f, hipMemcpyDeviceToHost, ix->stream));
     BSR_HIP(hipStreamSynchronize(ix->stream));
-    ix->row_flags = f;
-    if (f & kRowNonFinite) {
+    ix->row_flags = f[0];
+    memcpy(&ix->row_ebound, &f[1], sizeof(float));
+    if (f[0] & kRowNonFinite) {
         ix->loaded = false;
         ix->n = 0;
         return set_error(BSR_E_NONFINITE, "corpus contains NaN/Inf (the reference panics on NaN distances)");
     }
-    ix->approx_ok = !(f & (kRowNormOvf | kRowNormRange)) && !(ix->cfg.flags & BSR_FLAG_EXACT_ONLY);
+    ix->approx_ok = !(f[0] & (kRowNormOvf | kRowNormRange)) && !(ix->cfg.flags & BSR_FLAG_EXACT_ONLY);
     ix->loaded = true;
     return BSR_OK;
 }
@@ -179,6 +183,8 @@ int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
     ix->device = dev;
     ix->dim = cfg->dim;
     ix->ld = (uint32_t)round_up(cfg->dim, kLdAlign);
+    ix->op = (cfg->flags & BSR_FLAG_FILTER_BF16) ? kFilterBF16 : kFilterI8;
+    ix->op_row_bytes = ix->op == kFilterBF16 ? ix->ld * 2 : ix->ld;
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ix;
         return set_error(BSR_E_HIP, "hipStreamCreate failed");
@@ -285,6 +291,83 @@ static int run_exact_scan(bsr_index* ix, const std::vector<int32_t>& ids, uint32
     return BSR_OK;
 }
 
+// Candidate stage (steps 2-5) for every query of the batch.
+static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
+    const uint32_t kp = 64u * ((k + 54u + 63u) / 64u) - 1u;  // k' candidates, (k'+1) % 64 == 0
+    const uint32_t cap = 16u * (kp + 1u);
+    const uint32_t ks = (kp + 1u) / 8u;
+    const uint32_t BM = kFilterTile;
+    const uint64_t n = ix->n;
+    ix->stats.n_candidates = kp;
+    BSR_TRY(ix->tau.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(ix->cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
+    BSR_TRY(ix->cnt.ensure((size_t)qpad * sizeof(uint32_t)));
+    BSR_TRY(ix->cand_rows.ensure((size_t)nq * kp * sizeof(uint32_t)));
+    BSR_TRY(ix->ncand.ensure((size_t)nq * sizeof(uint32_t)));
+    BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));
+    BSR_TRY(ix->fail.ensure((size_t)nq * sizeof(uint32_t)));
+
+    GemmArgs g{};
+    g.A = ix->fop.as<uint8_t>();
+    g.B = ix->qop.as<uint8_t>();
+    g.row_bytes = ix->op_row_bytes;
+    g.n_qt = qpad / kFilterTile;
+    g.a_scale = ix->ascale.as<float>();
+    g.b_scale = ix->qscale.as<float>();
+    uint32_t* status = ix->status.as<uint32_t>();
+
+    if (n > cap) {
+        // tau0 from every 32nd row: the ks-th best sampled score, or (large shards) the
+        // ks-th best maximum over 32 sampled rows -- never above the former, so at least
+        // ~ks*32 rows of the shard reach it.
+        const uint32_t n_s = (uint32_t)((n + kSampleStride - 1) / kSampleStride);
+        const uint32_t n_rt_s = (n_s + BM - 1) / BM;
+        const bool compact = n_s >= 32u * 8u * ks;
+        const uint32_t s_ld = compact ? n_rt_s * (BM / 32) : n_rt_s * BM;
+        const uint32_t n_vals = compact ? (n_s + 31) / 32 : n_s;
+        BSR_TRY(ix->S.ensure((size_t)qpad * s_ld * sizeof(float)));
+        g.a_stride = (uint64_t)ix->op_row_bytes * kSampleStride;
+        g.a_row_mult = kSampleStride;
+        g.n_rows = n_s;
+        g.n_rt = n_rt_s;
+        g.S = ix->S.as<float>();
+        g.s_ld = s_ld;
+        g.s_compact = compact ? 1u : 0u;
+        ev_begin(ix, ix->ev_sample);
+        BSR_HIP(launch_filter_sample(ix->op, g, ix->stream));
+        ev_end(ix, ix->ev_sample);
+        BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
+                                  ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
+    } else {
+        BSR_HIP(launch_select_tau(nullptr, 0, 0, nq, qpad, ix->qflags.as<uint32_t>(), ks, ix->tau.as<float>(),
+                                  ix->cnt.as<uint32_t>(), status, ix->stream));
+    }
+    g.a_stride = ix->op_row_bytes;
+    g.a_row_mult = 1;
+    g.n_rows = (uint32_t)n;
+    g.n_rt = (uint32_t)((n + BM - 1) / BM);
+    g.S = nullptr;
+    g.tau = ix->tau.as<float>();
+    g.cand = ix->cand.as<uint64_t>();
+    g.cnt = ix->cnt.as<uint32_t>();
+    g.cap = cap;
+    ev_begin(ix, ix->ev_emit);
+    BSR_HIP(launch_filter_emit(ix->op, g, ix->stream));
+    ev_end(ix, ix->ev_emit);
+    ev_begin(ix, ix->ev_select);
+    BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(), kp,
+                               ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), ix->tau_excl.as<float>(),
+                               status, ix->stream));
+    ev_end(ix, ix->ev_select);
+    ev_begin(ix, ix->ev_rescore);
+    BSR_HIP(launch_rescore(ix->rows.as<float>(), ix->ld, ix->dim, ix->na.as<float>(), ix->qf32.as<float>(),
+                           ix->nb.as<float>(), nq, ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), kp,
+                           ix->tau_excl.as<float>(), k, ix->ebound.as<float>(), ix->keys.as<uint64_t>(), status,
+                           ix->fail.as<uint32_t>(), ix->stream));
+    ev_end(ix, ix->ev_rescore);
+    return BSR_OK;
+}
+
 int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     bsr_index* ix = this;
     if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
@@ -292,17 +375,22 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     BSR_HIP(hipSetDevice(ix->device));
     stats = bsr_search_stats{};
     stats.n_queries = nq;
+    stats.filter_op = (uint32_t)op;
+    stats.row_ebound = row_ebound;
     BSR_TRY(o_idx.ensure((size_t)std::max(nq, 1u) * k * sizeof(uint64_t)));
     BSR_TRY(o_dist.ensure((size_t)std::max(nq, 1u) * k * sizeof(float)));
     BSR_TRY(o_cnt.ensure((size_t)std::max(nq, 1u) * sizeof(uint32_t)));
     if (nq == 0) return BSR_OK;
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
 
-    const uint32_t qpad = (uint32_t)round_up(nq, gemm_query_pad());
+    const uint32_t qpad = (uint32_t)round_up(nq, kFilterTile);
     BSR_TRY(qf32.ensure((size_t)qpad * ld * sizeof(float)));
     BSR_TRY(nb.ensure((size_t)qpad * sizeof(float)));
-    BSR_TRY(qbf.ensure((size_t)qpad * ld * 2));
+    BSR_TRY(qop.ensure((size_t)qpad * op_row_bytes));
+    BSR_TRY(qscale.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(ebound.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(qflags.ensure((size_t)qpad * sizeof(uint32_t)));
+    BSR_TRY(status.ensure(kStWords * sizeof(uint32_t)));
     BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
 
     ev_begin(ix, ev_total);
@@ -312,110 +400,67 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
         qsrc = q_in.as<float>();
     }
-    BSR_HIP(launch_query_prep(qsrc, nq, qpad, dim, ld, qf32.as<float>(), nb.as<float>(), qbf.as<uint16_t>(),
-                              qflags.as<uint32_t>(), stream));
-    h_qflags.resize(nq);
-    BSR_HIP(hipMemcpyAsync(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    BSR_HIP(hipStreamSynchronize(stream));
-    std::vector<int32_t> exact_ids;
-    uint32_t n_eligible = 0;
-    for (uint32_t q = 0; q < nq; ++q) {
-        if (h_qflags[q] & kQueryNonFinite)
-            return set_error(BSR_E_NONFINITE, "query %u contains NaN/Inf (the reference panics)", q);
-        if (!(h_qflags[q] & kQueryNoApprox)) ++n_eligible;
-    }
+    BSR_HIP(hipMemsetAsync(status.p, 0, kStWords * sizeof(uint32_t), stream));
+    QueryPrepArgs qa{};
+    qa.q = qsrc;
+    qa.nq = nq;
+    qa.qpad = qpad;
+    qa.dim = dim;
+    qa.ld = ld;
+    qa.op = op;
+    qa.ea_max = flags.as<uint32_t>() + 1;
+    qa.qf32 = qf32.as<float>();
+    qa.nb = nb.as<float>();
+    qa.qop = qop.p;
+    qa.qscale = qscale.as<float>();
+    qa.ebound = ebound.as<float>();
+    qa.qflags = qflags.as<uint32_t>();
+    qa.status = status.as<uint32_t>();
+    BSR_HIP(launch_query_prep(qa, stream));
 
+    const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter && nq >= kMinBatchForFilter;
+    std::vector<int32_t> exact_ids;
     if (n == 0) {
         // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
         BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
+    } else if (!use_filter) {
+        for (uint32_t q = 0; q < nq; ++q) exact_ids.push_back((int32_t)q);
+        stats.n_exact_direct = nq;
+        BSR_TRY(run_exact_scan(ix, exact_ids, k));
     } else {
-        const bool use_filter = approx_ok && k <= kMaxKForFilter && n_eligible >= kMinBatchForFilter;
-        if (!use_filter) {
-            for (uint32_t q = 0; q < nq; ++q) exact_ids.push_back((int32_t)q);
-            stats.n_exact_direct = nq;
-            BSR_TRY(run_exact_scan(ix, exact_ids, k));
-        } else {
-            const uint32_t kp = 64u * ((k + 54u + 63u) / 64u) - 1u;  // k' candidates, (k'+1) % 64 == 0
-            const uint32_t cap = 16u * (kp + 1u);
-            const uint32_t ks = (kp + 1u) / 8u;
-            stats.n_candidates = kp;
-            BSR_TRY(tau.ensure((size_t)qpad * sizeof(float)));
-            BSR_TRY(cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
-            BSR_TRY(cnt.ensure((size_t)qpad * sizeof(uint32_t)));
-            BSR_TRY(cand_rows.ensure((size_t)nq * kp * sizeof(uint32_t)));
-            BSR_TRY(ncand.ensure((size_t)nq * sizeof(uint32_t)));
-            BSR_TRY(tau_excl.ensure((size_t)nq * sizeof(float)));
-            BSR_TRY(fail.ensure((size_t)(nq + 1) * sizeof(uint32_t)));
-
-            GemmArgs g{};
-            g.A = cbf.as<uint16_t>();
-            g.B = qbf.as<uint16_t>();
-            g.ld = ld;
-            g.n_qt = qpad / gemm_query_pad();
-            const uint32_t BM = gemm_row_tile();
-
-            uint32_t n_s = 0;
-            if (n > cap) {
-                n_s = (uint32_t)((n + kSampleStride - 1) / kSampleStride);
-                const uint32_t n_rt_s = (n_s + BM - 1) / BM;
-                const uint32_t s_ld = n_rt_s * BM;
-                BSR_TRY(S.ensure((size_t)qpad * s_ld * sizeof(float)));
-                g.a_row_stride = (uint64_t)ld * kSampleStride;
-                g.n_rows = n_s;
-                g.n_rt = n_rt_s;
-                g.S = S.as<float>();
-                g.s_ld = s_ld;
-                ev_begin(ix, ev_sample);
-                BSR_HIP(launch_gemm_sample(g, stream));
-                ev_end(ix, ev_sample);
-                BSR_HIP(launch_select_tau(S.as<float>(), s_ld, n_s, nq, qpad, qflags.as<uint32_t>(), ks,
-                                          tau.as<float>(), stream));
-            } else {
-                BSR_HIP(launch_select_tau(nullptr, 0, 0, nq, qpad, qflags.as<uint32_t>(), ks, tau.as<float>(),
-                                          stream));
-            }
-            BSR_HIP(hipMemsetAsync(cnt.p, 0, (size_t)qpad * sizeof(uint32_t), stream));
-            BSR_HIP(hipMemsetAsync(fail.p, 0, sizeof(uint32_t), stream));
-            g.a_row_stride = ld;
-            g.n_rows = (uint32_t)n;
-            g.n_rt = (uint32_t)((n + BM - 1) / BM);
-            g.tau = tau.as<float>();
-            g.cand = cand.as<uint64_t>();
-            g.cnt = cnt.as<uint32_t>();
-            g.cap = cap;
-            ev_begin(ix, ev_emit);
-            BSR_HIP(launch_gemm_emit(g, stream));
-            ev_end(ix, ev_emit);
-            ev_begin(ix, ev_select);
-            BSR_HIP(launch_select_cand(cand.as<uint64_t>(), cnt.as<uint32_t>(), cap, nq, tau.as<float>(), kp,
-                                       cand_rows.as<uint32_t>(), ncand.as<uint32_t>(), tau_excl.as<float>(), stream));
-            ev_end(ix, ev_select);
-            ev_begin(ix, ev_rescore);
-            BSR_HIP(launch_rescore(rows.as<float>(), ld, dim, na.as<float>(), qf32.as<float>(), nb.as<float>(), nq,
-                                   cand_rows.as<uint32_t>(), ncand.as<uint32_t>(), kp, tau_excl.as<float>(), k,
-                                   kEBound, keys.as<uint64_t>(), fail.as<uint32_t>(), fail.as<uint32_t>() + 1,
+        BSR_TRY(run_filter(ix, nq, qpad, k));
+    }
+    // The one status readback of the batch: non-finite queries, uncertified queries.
+    uint32_t st[kStWords] = {0, 0, 0, 0};
+    BSR_HIP(hipMemcpyAsync(st, status.p, sizeof st, hipMemcpyDeviceToHost, stream));
+    BSR_HIP(hipStreamSynchronize(stream));
+    if (st[kStQueryFlags] & kQueryNonFinite) {
+        h_qflags.resize(nq);
+        BSR_HIP(hipMemcpy(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        uint32_t bad = 0;
+        while (bad < nq && !(h_qflags[bad] & kQueryNonFinite)) ++bad;
+        return set_error(BSR_E_NONFINITE, "query %u contains NaN/Inf (the reference panics)", bad);
+    }
+    if (use_filter) {
+        stats.n_emitted = st[kStEmitted];
+        const uint32_t nfail = st[kStFail];
+        if (nfail) {
+            // Uncertified queries, and queries the filter cannot serve (zero/tiny/huge |b|),
+            // take the exact full scan: the reference's arithmetic on every row.
+            h_fail.resize(nfail);
+            h_qflags.resize(nq);
+            BSR_HIP(hipMemcpyAsync(h_fail.data(), fail.p, (size_t)nfail * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    stream));
-            ev_end(ix, ev_rescore);
-            uint32_t nfail = 0;
-            BSR_HIP(hipMemcpyAsync(&nfail, fail.p, sizeof nfail, hipMemcpyDeviceToHost, stream));
+            BSR_HIP(hipMemcpyAsync(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   stream));
             BSR_HIP(hipStreamSynchronize(stream));
-            if (profiling(ix)) {
-                // emitted-candidate count for diagnostics (cheap: qpad counters)
-                std::vector<uint32_t> c(nq);
-                BSR_HIP(hipMemcpy(c.data(), cnt.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
-                for (uint32_t v : c) stats.n_emitted += v;
+            std::sort(h_fail.begin(), h_fail.end());
+            for (uint32_t q : h_fail) {
+                exact_ids.push_back((int32_t)q);
+                if (h_qflags[q] & kQueryNoApprox) ++stats.n_exact_direct;
+                else ++stats.n_fallback;
             }
-            if (nfail) {
-                h_fail.resize(nfail);
-                BSR_HIP(hipMemcpy(h_fail.data(), fail.as<uint32_t>() + 1, (size_t)nfail * sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost));
-                std::sort(h_fail.begin(), h_fail.end());
-                for (uint32_t q : h_fail) exact_ids.push_back((int32_t)q);
-                for (uint32_t q : h_fail)
-                    if (!(h_qflags[q] & kQueryNoApprox)) ++stats.n_fallback;
-                stats.n_exact_direct = nfail - stats.n_fallback;
-                BSR_TRY(run_exact_scan(ix, exact_ids, k));
-            }
+            BSR_TRY(run_exact_scan(ix, exact_ids, k));
         }
     }
     BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, o_idx.as<uint64_t>(), o_dist.as<float>(),

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "bsr.h"
+#include "kernels.hpp"
 
 namespace bsr {
 
@@ -62,15 +63,19 @@ struct bsr_index {
     bool loaded = false;
     bool approx_ok = false;
     uint32_t row_flags = 0;
+    bsr::FilterOp op = bsr::kFilterI8;  // MFMA filter operand type (BSR_FLAG_FILTER_BF16)
+    uint32_t op_row_bytes = 0;          // bytes of one filter operand row
+    float row_ebound = 0.0f;            // int8: max_row ||a/|a| - s q||_2 (certification)
 
-    bsr::DevBuf rows;  // f32 [n_pad][ld], zero padded: the reference's values
-    bsr::DevBuf na;    // f32 [n_pad]: exact magnitudes (src/metrics.rs:154)
-    bsr::DevBuf cbf;   // bf16 [n_pad][ld]: normalised rows for the MFMA filter
-    bsr::DevBuf flags; // u32
+    bsr::DevBuf rows;   // f32 [n_pad][ld], zero padded: the reference's values
+    bsr::DevBuf na;     // f32 [n_pad]: exact magnitudes (src/metrics.rs:154)
+    bsr::DevBuf fop;    // filter operand rows: int8 or bf16 [n_pad][ld]
+    bsr::DevBuf ascale; // int8: f32 [n_pad/32] block scales
+    bsr::DevBuf flags;  // u32 [2]: row flags, int8 row error bound (f32 bits)
 
     // per-search scratch
-    bsr::DevBuf q_in, qf32, nb, qbf, qflags, tau, S, cand, cnt, cand_rows, ncand, tau_excl, keys,
-        fail, part, qids, o_idx, o_dist, o_cnt, tmp;
+    bsr::DevBuf q_in, qf32, nb, qop, qscale, ebound, qflags, status, tau, S, cand, cnt, cand_rows,
+        ncand, tau_excl, keys, fail, part, qids, o_idx, o_dist, o_cnt, tmp;
     std::vector<uint32_t> h_qflags, h_fail;
 
     bsr_search_stats stats{};

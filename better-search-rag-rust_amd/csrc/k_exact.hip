@@ -1,0 +1,408 @@
+// k_exact.hip -- the reference's exact arithmetic on the GPU (gfx950): candidate rescoring
+// with certification, the exact full scan, per-block list merges and output finalisation.
+//
+// Compiled with -ffp-contract=off: every f32 multiply and add rounds separately, in index
+// order, exactly as src/metrics.rs:153-155 does; sqrt is __builtin_sqrtf (correctly
+// rounded) and `/` is the correctly rounded division (see bsr_device.hpp).
+#include "bsr_device.hpp"
+#include "kernels.hpp"
+
+#include <math.h>
+
+namespace bsr {
+
+static inline uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap = 65536) {
+    uint64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    return (uint32_t)(g > cap ? cap : g);
+}
+
+// ------------------------------------------------------------------------------------
+// Exact rescoring of the candidates (one wave per query, lane = candidate): the row and the
+// query are walked in index order with separate f32 multiply/add, chunks of 64 elements
+// staged through LDS (rows padded to 68 floats: conflict-free ds_read_b128).  The final
+// top-k list is certified against the MFMA filter's error bound.
+// ------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+// Loads of one 64-element chunk of 64 candidate rows (16 x 16 B per lane; each
+// wave-instruction covers 4 rows x 256 B).
+__device__ __forceinline__ void load_cand_chunk(f32x4_t (&pre)[16], const float* __restrict__ rows,
+                                                uint32_t ld, const uint32_t (&lrow)[16], uint32_t ch,
+                                                int lane) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        pre[i] = *reinterpret_cast<const f32x4_t*>(rows + (uint64_t)lrow[i] * ld + ch * 64 + (lane & 15) * 4);
+}
+
+// One 64-element chunk of 64 rows held in LDS (stride 68 floats), walked in index order by
+// the lane that owns the row: sequential dot (separate f32 mul and add) and max|a_i - b_i|.
+template <int QF>
+__device__ __forceinline__ void seq_chunk(const float* __restrict__ my, const float* const (&bq)[QF],
+                                          uint32_t nvalid, float (&acc)[QF], float (&mx)[QF]) {
+    if (nvalid == 64) {
+#pragma unroll
+        for (int i = 0; i < 64; i += 4) {
+            const f32x4_t a = *reinterpret_cast<const f32x4_t*>(my + i);
+#pragma unroll
+            for (int j = 0; j < QF; ++j) {
+                const float* bb = bq[j] + i;
+                acc[j] = acc[j] + a.x * bb[0]; mx[j] = fmaxf(mx[j], fabsf(a.x - bb[0]));
+                acc[j] = acc[j] + a.y * bb[1]; mx[j] = fmaxf(mx[j], fabsf(a.y - bb[1]));
+                acc[j] = acc[j] + a.z * bb[2]; mx[j] = fmaxf(mx[j], fabsf(a.z - bb[2]));
+                acc[j] = acc[j] + a.w * bb[3]; mx[j] = fmaxf(mx[j], fabsf(a.w - bb[3]));
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < nvalid; ++i) {
+            const float a = my[i];
+#pragma unroll
+            for (int j = 0; j < QF; ++j) {
+                const float bv = bq[j][i];
+                acc[j] = acc[j] + a * bv;
+                mx[j] = fmaxf(mx[j], fabsf(a - bv));
+            }
+        }
+    }
+}
+
+template <int E>
+__global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, uint32_t ld, uint32_t dim,
+                                                const float* __restrict__ na, const float* __restrict__ qf32,
+                                                const float* __restrict__ nb, uint32_t nq,
+                                                const uint32_t* __restrict__ cand_rows,
+                                                const uint32_t* __restrict__ ncand, uint32_t kp,
+                                                const float* __restrict__ tau_excl, uint32_t k,
+                                                const float* __restrict__ ebound_q,
+                                                uint64_t* __restrict__ out_keys,
+                                                uint32_t* __restrict__ status,
+                                                uint32_t* __restrict__ fail_list) {
+    __shared__ __attribute__((aligned(16))) float lds[64 * 68];
+    const uint32_t q = blockIdx.x;
+    if (q >= nq) return;
+    const int lane = threadIdx.x;
+    const uint32_t c = ncand[q];
+    const float* bq = qf32 + (uint64_t)q * ld;
+    const float mag_b = nb[q];
+    const uint32_t nch = ld / 64;
+
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    for (uint32_t base = 0; base < c; base += kWave) {
+        const uint32_t ci = base + lane;
+        const uint32_t myrow = cand_rows[(uint64_t)q * kp + (ci < c ? ci : 0)];
+        float acc[1] = {-0.0f}, mx[1] = {0.0f};
+        uint32_t lrow[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
+        f32x4_t pre[16];
+        load_cand_chunk(pre, rows, ld, lrow, 0, lane);
+        for (uint32_t ch = 0; ch < nch; ++ch) {
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int L16 = i * 64 + lane;
+                *reinterpret_cast<f32x4_t*>(lds + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
+            }
+            __syncthreads();
+            load_cand_chunk(pre, rows, ld, lrow, ch + 1 < nch ? ch + 1 : ch, lane);  // clamped prefetch
+            const float* const bb[1] = {bq + ch * 64};
+            const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
+            seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
+        }
+        const float d = finish_distance(acc[0], mx[0], na[myrow], mag_b);
+        L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)k, thr);
+    }
+    L.store(out_keys + (uint64_t)q * k, (int)k);
+
+    if (lane == 0) {
+        // Certification: every row outside the candidate set has approximate
+        // cosine <= tau_x, hence reference cosine <= tau_x + E_q and reference distance
+        // >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must lie strictly below
+        // that, and no excluded row can be element-wise identical to the query.
+        const float tx = tau_excl[q];
+        const double ebound = (double)ebound_q[q];
+        bool ok;
+        if (tx == -INFINITY) {
+            ok = true;  // every row of the shard was a candidate
+        } else if (!(tx < INFINITY) || thr == kKeyNone) {
+            ok = false;
+        } else {
+            const double dk = (double)key_dist(thr);
+            ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
+                 (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
+        }
+        if (!ok) {
+            const uint32_t pos = atomicAdd(status + kStFail, 1u);
+            fail_list[pos] = q;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Exact full scan (src/mpi_helpers/metrics.rs:36-50 for up to QF queries at once): 256
+// rows per tile (lane = row), 64-element chunks of the row-major slab staged through LDS
+// (padded to 68 floats: conflict-free ds_read_b128), next chunk prefetched into registers.
+// Each lane walks its row in index order per query: sequential dot, max|a_i-b_i|.  Per
+// wave a sorted top-k per query; the 4 waves merge through LDS into one list per block.
+// ------------------------------------------------------------------------------------
+template <int QF, int E>
+__global__ __launch_bounds__(256, 2) void k_scan_exact(const float* __restrict__ rows, uint32_t ld,
+                                                       uint32_t dim, uint64_t n,
+                                                       const float* __restrict__ na,
+                                                       const float* __restrict__ qf32,
+                                                       const int32_t* __restrict__ qids,
+                                                       const float* __restrict__ nb, uint32_t k,
+                                                       uint64_t* __restrict__ part) {
+    // rows [256][68] + (QF > 1) query chunk [QF][64]; QF == 1 reads the query through the
+    // scalar cache instead (64 SGPRs per chunk), QF > 1 would spill SGPRs.
+    __shared__ __attribute__((aligned(16))) float lds[256 * 68 + (QF > 1 ? QF * 64 : 0)];
+    float* ldq = lds + 256 * 68;
+    const int t = threadIdx.x, w = t >> 6;
+    const uint64_t n_tiles = (n + 255) / 256;
+    const uint32_t nch = ld / 64;
+
+    const float* qp[QF];
+    float mag_b[QF];
+#pragma unroll
+    for (int j = 0; j < QF; ++j) {
+        const int32_t id = qids[j];
+        qp[j] = qf32 + (uint64_t)id * ld;
+        mag_b[j] = nb[id];
+    }
+    WaveTopK<E> L[QF];
+    uint64_t thr[QF];
+#pragma unroll
+    for (int j = 0; j < QF; ++j) { L[j].init(); thr[j] = kKeyNone; }
+
+    // This lane's 16 load addresses within a tile chunk: row (i*256+t)>>4, float4 (t&15).
+    const uint32_t lrow0 = (uint32_t)t >> 4;   // + 16*i
+    const uint32_t lcol = ((uint32_t)t & 15) * 4;
+    uint64_t tile = blockIdx.x;
+    uint32_t ch = 0;
+    f32x4_t pre[16];
+    f32x4_t qpre = {0.0f, 0.0f, 0.0f, 0.0f};
+    // thread t < QF*16 also stages float4 (t&15) of query t>>4's chunk
+    const float* qsrc = (QF > 1 && t < QF * 16) ? qp[QF > 1 ? (t >> 4) % QF : 0] + lcol : nullptr;
+    auto issue = [&](uint64_t tl, uint32_t c) {
+        const float* base = rows + (tl * 256 + lrow0) * ld + c * 64 + lcol;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pre[i] = *reinterpret_cast<const f32x4_t*>(base + (uint64_t)i * 16 * ld);
+        if constexpr (QF > 1) {
+            if (qsrc) qpre = *reinterpret_cast<const f32x4_t*>(qsrc + c * 64);
+        }
+    };
+    if (tile < n_tiles) issue(tile, 0);
+    float acc[QF], mx[QF];
+#pragma unroll
+    for (int j = 0; j < QF; ++j) { acc[j] = -0.0f; mx[j] = 0.0f; }
+
+    while (tile < n_tiles) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            *reinterpret_cast<f32x4_t*>(lds + (lrow0 + 16 * i) * 68 + lcol) = pre[i];
+        if constexpr (QF > 1) {
+            if (qsrc) *reinterpret_cast<f32x4_t*>(ldq + (t >> 4) * 64 + lcol) = qpre;
+        }
+        __syncthreads();
+        // next (tile, chunk); past the end: reload the current chunk (branch-free prefetch)
+        uint64_t ntile = tile;
+        uint32_t nch_ = ch + 1;
+        if (nch_ == nch) { nch_ = 0; ntile = tile + gridDim.x; }
+        if (ntile >= n_tiles) { ntile = tile; nch_ = ch; }
+        issue(ntile, nch_);
+
+        const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
+        const float* bq[QF];
+#pragma unroll
+        for (int j = 0; j < QF; ++j) bq[j] = (QF > 1) ? ldq + j * 64 : qp[j] + ch * 64;
+        seq_chunk<QF>(lds + t * 68, bq, nvalid, acc, mx);
+
+        if (ch == nch - 1) {
+            const uint64_t row = tile * 256 + t;
+            const bool valid = row < n;
+            const float mag_a = valid ? na[row] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < QF; ++j) {
+                const float d = finish_distance(acc[j], mx[j], mag_a, mag_b[j]);
+                L[j].offer(valid ? dist_key(d, (uint32_t)row) : kKeyNone, (int)k, thr[j]);
+                acc[j] = -0.0f;
+                mx[j] = 0.0f;
+            }
+            ch = 0;
+            tile += gridDim.x;
+        } else {
+            ++ch;
+        }
+    }
+
+    // Block merge: 4 wave lists per query -> one list per query.
+    __syncthreads();
+    uint64_t* lk = reinterpret_cast<uint64_t*>(lds);  // [4][QF][64E] keys (<= 64 KiB)
+#pragma unroll
+    for (int j = 0; j < QF; ++j) L[j].store(lk + ((uint64_t)w * QF + j) * 64 * E, (int)k);
+    __syncthreads();
+    for (int j = w; j < QF; j += 4) {
+        WaveTopK<E> M;
+        M.init();
+        uint64_t mt = kKeyNone;
+        for (int s = 0; s < 4; ++s) {
+            const uint64_t* src = lk + ((uint64_t)s * QF + j) * 64 * E;
+            for (uint32_t base = 0; base < k; base += kWave) {
+                const uint32_t i = base + (t & 63);
+                M.offer(i < k ? src[i] : kKeyNone, (int)k, mt);
+            }
+        }
+        M.store(part + ((uint64_t)blockIdx.x * QF + j) * k, (int)k);
+    }
+}
+
+// Per scanned query: merge the per-block lists of k_scan_exact into out_keys[qid].
+template <int E>
+__global__ __launch_bounds__(64) void k_merge_parts(const uint64_t* __restrict__ part, uint32_t grid,
+                                                    const int32_t* __restrict__ qids, uint32_t qf,
+                                                    uint32_t nqf, uint32_t k,
+                                                    uint64_t* __restrict__ out_keys) {
+    const uint32_t j = blockIdx.x;
+    if (j >= nqf) return;
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    const uint64_t total = (uint64_t)grid * k;
+    for (uint64_t base = 0; base < total; base += kWave) {
+        const uint64_t i = base + threadIdx.x;
+        uint64_t key = kKeyNone;
+        if (i < total) {
+            const uint64_t g = i / k, e = i - g * k;
+            key = part[(g * qf + j) * k + e];
+        }
+        L.offer(key, (int)k, thr);
+    }
+    L.store(out_keys + (uint64_t)qids[j] * k, (int)k);
+}
+
+__global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint64_t n,
+                           uint64_t offset, uint64_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                           uint32_t* __restrict__ out_count) {
+    const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (e >= (uint64_t)nq * k) return;
+    const uint32_t q = (uint32_t)(e / k), i = (uint32_t)(e - (uint64_t)q * k);
+    const uint32_t cnt = (uint64_t)k < n ? k : (uint32_t)n;
+    const uint64_t key = keys[e];
+    if (i < cnt && key != kKeyNone) {
+        out_idx[e] = offset + key_row(key);
+        out_dist[e] = key_dist(key);
+    } else {
+        out_idx[e] = ~0ull;
+        out_dist[e] = INFINITY;
+    }
+    if (i == 0) out_count[q] = cnt;
+}
+
+// src/metrics.rs:143-165 for one pair (single lane, fully sequential, from global memory).
+__global__ void k_cosine_pair(const float* __restrict__ a, uint32_t la, const float* __restrict__ b,
+                              uint32_t lb, float* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (la != lb || la == 0) { *out = 1.0f; return; }
+    float dot = -0.0f, aa = -0.0f, bb = -0.0f, mx = 0.0f;
+    for (uint32_t i = 0; i < la; ++i) {
+        const float x = a[i], y = b[i];
+        mx = fmaxf(mx, fabsf(x - y));
+        dot = dot + x * y;
+        aa = aa + x * x;
+        bb = bb + y * y;
+    }
+    *out = finish_distance(dot, mx, __builtin_sqrtf(aa), __builtin_sqrtf(bb));
+}
+
+// ------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------
+hipError_t launch_rescore(const float* rows, uint32_t ld, uint32_t dim, const float* na, const float* qf32,
+                          const float* nb, uint32_t nq, const uint32_t* cand_rows, const uint32_t* ncand,
+                          uint32_t kp, const float* tau_excl, uint32_t k, const float* ebound, uint64_t* out_keys,
+                          uint32_t* status, uint32_t* fail_list, hipStream_t s) {
+    const uint32_t e = (k + 63) / 64;
+#define BSR_RESCORE(E)                                                                              \
+    hipLaunchKernelGGL(k_rescore<E>, dim3(nq), dim3(64), 0, s, rows, ld, dim, na, qf32, nb, nq,   \
+                       cand_rows, ncand, kp, tau_excl, k, ebound, out_keys, status, fail_list)
+    switch (e) {
+        case 1: BSR_RESCORE(1); break;
+        case 2: BSR_RESCORE(2); break;
+        case 3: BSR_RESCORE(3); break;
+        case 4: BSR_RESCORE(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef BSR_RESCORE
+    return hipGetLastError();
+}
+
+uint32_t scan_grid_for(uint64_t n) {
+    const uint64_t tiles = (n + 255) / 256;
+    const uint64_t g = tiles < 512 ? tiles : 512;  // 2 blocks per CU x 256 CUs
+    return (uint32_t)(g < 1 ? 1 : g);
+}
+
+template <int QF>
+static void launch_scan_qf(const float* rows, uint32_t ld, uint32_t dim, uint64_t n, const float* na,
+                           const float* qf32, const int32_t* qids, const float* nb, uint32_t k,
+                           uint32_t grid, uint64_t* part, hipStream_t s) {
+    const uint32_t e = (k + 63) / 64;
+#define BSR_SCAN(E)                                                                                  \
+    hipLaunchKernelGGL((k_scan_exact<QF, E>), dim3(grid), dim3(256), 0, s, rows, ld, dim, n, na,  \
+                       qf32, qids, nb, k, part)
+    switch (e) {
+        case 1: BSR_SCAN(1); break;
+        case 2: BSR_SCAN(2); break;
+        case 3: BSR_SCAN(3); break;
+        default: BSR_SCAN(4); break;
+    }
+#undef BSR_SCAN
+}
+
+hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint64_t n, const float* na,
+                             const float* qf32, const int32_t* qids, uint32_t nqf, const float* nb,
+                             uint32_t k, uint32_t grid, uint64_t* part, hipStream_t s) {
+    // Query ids beyond nqf must be valid (the caller repeats the last id); results for them
+    // are computed and ignored.
+    if (nqf <= 1) launch_scan_qf<1>(rows, ld, dim, n, na, qf32, qids, nb, k, grid, part, s);
+    else if (nqf <= 2) launch_scan_qf<2>(rows, ld, dim, n, na, qf32, qids, nb, k, grid, part, s);
+    else if (nqf <= 4) launch_scan_qf<4>(rows, ld, dim, n, na, qf32, qids, nb, k, grid, part, s);
+    else launch_scan_qf<8>(rows, ld, dim, n, na, qf32, qids, nb, k, grid, part, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t* qids, uint32_t nqf,
+                              uint32_t k, uint64_t* out_keys, hipStream_t s) {
+    const uint32_t qf = nqf <= 1 ? 1 : nqf <= 2 ? 2 : nqf <= 4 ? 4 : 8;
+    const uint32_t e = (k + 63) / 64;
+#define BSR_MERGE(E)                                                                              \
+    hipLaunchKernelGGL(k_merge_parts<E>, dim3(nqf), dim3(64), 0, s, part, grid, qids, qf, nqf, k, \
+                       out_keys)
+    switch (e) {
+        case 1: BSR_MERGE(1); break;
+        case 2: BSR_MERGE(2); break;
+        case 3: BSR_MERGE(3); break;
+        default: BSR_MERGE(4); break;
+    }
+#undef BSR_MERGE
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n, uint64_t offset,
+                           uint64_t* out_idx, float* out_dist, uint32_t* out_count, hipStream_t s) {
+    const uint64_t total = (uint64_t)nq * k;
+    hipLaunchKernelGGL(k_finalize, dim3(grid_for(total, 256)), dim3(256), 0, s, keys, nq, k, n, offset,
+                       out_idx, out_dist, out_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_cosine_pair(const float* a, uint32_t la, const float* b, uint32_t lb, float* out,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_cosine_pair, dim3(1), dim3(64), 0, s, a, la, b, lb, out);
+    return hipGetLastError();
+}
+
+}  // namespace bsr

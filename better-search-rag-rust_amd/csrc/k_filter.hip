@@ -1,0 +1,504 @@
+// k_filter.hip -- the MFMA candidate filter of the search (gfx950) and its selection steps.
+//
+// The filter scores every (corpus row, query) pair approximately on the matrix cores and
+// keeps the pairs that can belong to a query's top k.  It never produces a returned
+// distance: the candidates are rescored with the reference's exact arithmetic
+// (k_exact.hip) and the final list is certified against the filter's error bound.
+//
+// Two operand types share one kernel (template Op):
+//   OpI8   int8 rows (per 32-row block scale) x int8 queries (per query scale) on
+//          v_mfma_i32_32x32x32_i8; the integer dot product is exact, the score is
+//          ((float)I * s_row_block) * s_query.
+//   OpBF16 bf16(a/|a|) x bf16(b/|b|) on v_mfma_f32_32x32x16_bf16.
+// Both move 64 bytes of K per row per slice, so the tiling, the LDS ring and the issue
+// schedule are identical; an int8 slice carries twice the K of a bf16 slice.
+#include "bsr_device.hpp"
+#include "kernels.hpp"
+
+#include <math.h>
+
+namespace bsr {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+typedef __attribute__((ext_vector_type(16))) int i32x16_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+struct OpBF16 {
+    using frag_t = bf16x8_t;
+    using acc_t = f32x16_t;
+    static constexpr bool kInt = false;
+    __device__ __forceinline__ static acc_t mfma(const frag_t& a, const frag_t& b, const acc_t& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+struct OpI8 {
+    using frag_t = i32x4_t;
+    using acc_t = i32x16_t;
+    static constexpr bool kInt = true;
+    __device__ __forceinline__ static acc_t mfma(const frag_t& a, const frag_t& b, const acc_t& c) {
+        return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+    }
+};
+
+constexpr int kSlots = 4;     // LDS ring slots (3 slices in flight + the one being read)
+constexpr int kSliceB = 64;   // bytes of K per row per slice
+constexpr int kWCap = 256;    // candidate buffer entries per wave (one is the counter)
+constexpr int kThreads = 512; // 8 waves: 2 (rows) x 4 (queries)
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Mid-slice barrier: the slice the next fragment reads come from has landed for every
+// wave (counted vmcnt: the N youngest LDS-DMA stay in flight), and this wave's fragment
+// reads are complete (the slot they read may be refilled after the barrier).
+template <int N>
+__device__ __forceinline__ void mid_barrier() {
+    if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------
+// The filter.  Persistent workgroups (512 threads, waves 2 x 4, each wave 128 rows x 64
+// queries = 4 x 2 blocks of 32 x 32), each owning one 256-query tile for its life
+// (thresholds and query scales in registers) and walking 256-row corpus tiles g, g+RG, ...;
+// the n_qt workgroups that share a row tile share an XCD (blockIdx % 8), so each row tile
+// leaves HBM once per XCD.  Operands arrive by global_load_lds_dwordx4 into a 4-slot ring
+// of 64-byte K slices (32 KiB per slot, 3 slices in flight), XOR-swizzled on the source
+// address so that every ds_read_b128 fragment read is conflict-free.  Issue order per
+// slice j (F0/F1 = fragment register sets of the two K sub-steps):
+//   [F1 <- ds_read(j, kk=1)] 4 MFMA(F0) dma(j+3,A0) 4 MFMA(F0) dma(j+3,A1)
+//   s_waitcnt lgkmcnt(0) vmcnt(N) ; s_barrier          <- slice j+1 landed everywhere
+//   [F0 <- ds_read(j+1, kk=0)] 4 MFMA(F1) dma(j+3,B0) 4 MFMA(F1) dma(j+3,B1)
+// The barrier sits mid-slice: the slot a DMA overwrites (slice j-1) was last read before
+// the previous barrier.  sched_barrier(0) pins the placement against the scheduler.
+//
+// Epilogue per 32x32 block (EMIT): the block maximum against the query's threshold tau
+// (one ballot), then only the passing (lane, register) pairs append (score, row) keys to
+// a per-wave LDS buffer (inline-asm ds_add_rtn; hipcc would drain vmcnt before a plain LDS
+// atomic), flushed to the per-query global lists at the end.  int8: the block scales of
+// the current tile are fetched into this wave's LDS words by a 4-lane LDS-DMA issued with
+// the tile's first slice and covered by the counted waits two slices later.
+// SAMPLE (!EMIT): every tile row is one sampled corpus row; the scores go to S, either
+// all of them (s_compact == 0) or one maximum per 32 sampled rows (s_compact == 1).
+//
+// VAR (tooling, tools/microbench): 1 = no LDS-DMA in the loop (compute ceiling),
+// 3 = LDS-DMA, waits and barriers only (operand-feed ceiling), 4 = A always the same tile.
+// ------------------------------------------------------------------------------------
+template <class Op, bool EMIT, int VAR = 0>
+__global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
+    using frag_t = typename Op::frag_t;
+    using acc_t = typename Op::acc_t;
+    constexpr int BM = kFilterTile, BN = kFilterTile;
+    constexpr int A_BYTES = BM * kSliceB, B_BYTES = BN * kSliceB;
+    constexpr int SLOT = A_BYTES + B_BYTES;
+    constexpr int EM_BYTES = EMIT ? 8 * kWCap * 12 : 0;
+    constexpr bool kScaleDMA = EMIT && Op::kInt;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[kSlots * SLOT + EM_BYTES + (kScaleDMA ? 8 * 16 : 0)];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 2, wc = w & 3;
+    uint64_t* ekeys = reinterpret_cast<uint64_t*>(lds + kSlots * SLOT) + w * kWCap;
+    uint32_t* eq = reinterpret_cast<uint32_t*>(lds + kSlots * SLOT + 8 * kWCap * 8) + w * kWCap;
+    float* lsc = reinterpret_cast<float*>(lds + kSlots * SLOT + EM_BYTES) + w * 4;
+    // per-wave append counter: the last q slot of the wave's region (capacity kWCap-1)
+    const uint32_t ecnt_addr = (uint32_t)(uintptr_t)(eq + kWCap - 1);
+    if (EMIT && lane == 0) eq[kWCap - 1] = 0;
+
+    const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const uint32_t G = (gridDim.x >> 3) / p.n_qt;
+    const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
+    const uint32_t nk = p.row_bytes / kSliceB;
+    const bool active = slot < G * p.n_qt;
+    const uint32_t qt = active ? slot % p.n_qt : 0;
+    const uint32_t g0 = xcd * G + (active ? slot / p.n_qt : 0);
+    const uint32_t RG = 8 * G;
+    const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
+    const uint32_t J = my_rt * nk;
+
+    uint32_t lrow[2], lchunk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        lrow[i] = (w * 2 + i) * 16 + (lane >> 2);
+        lchunk[i] = (lane & 3) ^ ((lrow[i] >> 2) & 3);
+    }
+    const uint8_t* bsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) bsrc[i] = p.B + (uint64_t)(qt * BN + lrow[i]) * p.row_bytes + lchunk[i] * 16;
+    const uint64_t a_lane_off[2] = {(uint64_t)lrow[0] * p.a_stride + lchunk[0] * 16,
+                                    (uint64_t)lrow[1] * p.a_stride + lchunk[1] * 16};
+    // DMA pointers of the slice being issued (slice jj+3), advanced incrementally.
+    uint32_t iss_ti = 0, iss_kt = 0;
+    const uint8_t* a_tile = p.A;
+    auto set_issue_tile = [&]() {
+        const uint32_t rt = VAR == 4 ? g0 : g0 + iss_ti * RG;
+        a_tile = p.A + (uint64_t)rt * BM * p.a_stride;
+    };
+    auto dma_a = [&](uint32_t jj, int i) {
+        uint8_t* la = lds + (jj % kSlots) * SLOT;
+        const uint8_t* src = a_tile + a_lane_off[i] + iss_kt * kSliceB;
+        if (!EMIT) {  // sample pass: clamp tail rows to the last valid one
+            const uint32_t rt = g0 + iss_ti * RG;
+            if (rt * BM + lrow[i] >= p.n_rows)
+                src = p.A + (uint64_t)(p.n_rows - 1) * p.a_stride + lchunk[i] * 16 + iss_kt * kSliceB;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(la + (w * 2 + i) * 1024), 16, 0, 0);
+    };
+    auto dma_b = [&](uint32_t jj, int i) {
+        uint8_t* lb = lds + (jj % kSlots) * SLOT + A_BYTES;
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + iss_kt * kSliceB),
+                                         (lds_void_t*)(lb + (w * 2 + i) * 1024), 16, 0, 0);
+    };
+    auto issue_advance = [&]() {
+        if (++iss_kt == nk) { iss_kt = 0; ++iss_ti; set_issue_tile(); }
+    };
+
+    int aoff[4][2], boff[2][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int row = wr * 128 + m * 32 + (lane & 31);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int lc = 2 * kk + (lane >> 5);
+            aoff[m][kk] = row * kSliceB + ((lc ^ ((row >> 2) & 3)) * 16);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const int row = wc * 64 + n * 32 + (lane & 31);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int lc = 2 * kk + (lane >> 5);
+            boff[n][kk] = A_BYTES + row * kSliceB + ((lc ^ ((row >> 2) & 3)) * 16);
+        }
+    }
+    float tau[2] = {0.0f, 0.0f}, sbq[2] = {1.0f, 1.0f};
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const uint32_t q = qt * BN + wc * 64 + n * 32 + (lane & 31);
+        if (EMIT) tau[n] = p.tau[q];
+        if (Op::kInt) sbq[n] = p.b_scale[q];
+    }
+
+    acc_t acc[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+
+    frag_t fa0[4], fb0[2], fa1[4], fb1[2];
+    auto read_frags = [&](uint32_t jj, int kk, frag_t (&fa)[4], frag_t (&fb)[2]) {
+        if constexpr (VAR >= 3) return;
+        const uint8_t* base = lds + (VAR == 1 ? 0 : jj % kSlots) * SLOT;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) fa[m] = *reinterpret_cast<const frag_t*>(base + aoff[m][kk]);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) fb[n] = *reinterpret_cast<const frag_t*>(base + boff[n][kk]);
+    };
+    auto mfma4 = [&](const frag_t (&fa)[4], const frag_t (&fb)[2], int half) {
+        if constexpr (VAR >= 3) return;
+#pragma unroll
+        for (int m = half * 2; m < half * 2 + 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) acc[m][n] = Op::mfma(fa[m], fb[n], acc[m][n]);
+    };
+    // The score of accumulator element v of block m (int8: exact integer dot, then the two
+    // scale multiplies in this fixed order; the candidate keys use the same expression).
+    auto score = [&](auto v, float sc_m, int n) -> float {
+        if constexpr (Op::kInt) return ((float)v * sc_m) * sbq[n];
+        else return v;
+    };
+
+    // Prologue: slices 0..min(J,3)-1 issued; wait for slice 0; F0 <- (0, kk=0).
+    set_issue_tile();
+    const uint32_t pre = J < 3 ? J : 3;
+    for (uint32_t jj = 0; jj < pre; ++jj) {
+        dma_a(jj, 0); dma_a(jj, 1); dma_b(jj, 0); dma_b(jj, 1);
+        issue_advance();
+    }
+    if (pre == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (pre == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (J) read_frags(0, 0, fa0, fb0);
+
+    uint32_t ti = 0, kt = 0;
+    for (uint32_t jj = 0; jj < J; ++jj) {
+        const bool iss = VAR != 1 && jj + 3 < J;
+        // ---- first half: kk = 0 MFMAs, kk = 1 reads, A-half DMA of slice jj+3
+        read_frags(jj, 1, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa0, fb0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (iss) dma_a(jj + 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa0, fb0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (iss) dma_a(jj + 3, 1);
+        if constexpr (kScaleDMA) {
+            // this wave's 4 block scales of the current tile (rows rt*256 + wr*128 + 32m);
+            // younger than every slice DMA in flight, so covered two mid-barriers later
+            if (kt == 0 && lane < 4) {
+                const uint32_t blk = ((g0 + ti * RG) * BM + wr * 128) / kQuantBlock + lane;
+                __builtin_amdgcn_global_load_lds((const void*)(p.a_scale + blk), (lds_void_t*)lsc, 4, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- mid-slice barrier: slice jj+1 has landed for every wave
+        if (VAR == 1) {
+            mid_barrier<8>();
+        } else if (jj + 3 < J) {
+            mid_barrier<6>();
+        } else if (jj + 2 < J) {
+            mid_barrier<4>();
+        } else {
+            mid_barrier<0>();
+        }
+        const bool next = jj + 1 < J;
+        if (next) read_frags(jj + 1, 0, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa1, fb1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (iss) dma_b(jj + 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa1, fb1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (iss) { dma_b(jj + 3, 1); issue_advance(); }
+        __builtin_amdgcn_sched_barrier(0);
+
+        if (kt == nk - 1) {
+            const uint32_t rt = g0 + ti * RG;
+            bool stored = false;
+            float sc[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+            if constexpr (kScaleDMA) {
+                if (nk < 3) wait_vm0();  // fewer than two barriers since the scale DMA
+#pragma unroll
+                for (int m = 0; m < 4; ++m) sc[m] = lsc[m];
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    const uint32_t ql = wc * 64 + n * 32 + (lane & 31);
+                    const uint32_t rbase = rt * BM + wr * 128 + m * 32 + 4 * (lane >> 5);
+                    if constexpr (!EMIT) {
+                        // sample scores: tile row r is corpus row r * a_row_mult
+                        float v[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            float s_r = 1.0f;
+                            if constexpr (Op::kInt) {
+                                uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
+                                tr = tr < p.n_rows ? tr : p.n_rows - 1;
+                                s_r = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                            }
+                            v[r] = score(acc[m][n][r], s_r, n);
+                        }
+                        float* srow = p.S + (uint64_t)(qt * BN + ql) * p.s_ld;
+                        if (!p.s_compact) {  // full: every sampled row
+#pragma unroll
+                            for (int g = 0; g < 4; ++g)
+                                *reinterpret_cast<float4*>(srow + rbase + 8 * g) =
+                                    make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+                        } else {  // compact: one maximum per 32 sampled rows
+                            float mx = v[0];
+#pragma unroll
+                            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, v[r]);
+                            mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                            if (lane < 32) srow[(rt * BM + wr * 128 + m * 32) / 32] = mx;
+                        }
+                        stored = true;
+                    } else {
+                        auto mxv = acc[m][n][0];
+#pragma unroll
+                        for (int r = 1; r < 16; ++r) mxv = mxv > acc[m][n][r] ? mxv : acc[m][n][r];
+                        if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
+                            uint32_t mask = 0;
+#pragma unroll
+                            for (int r = 0; r < 16; ++r)
+                                mask |= (score(acc[m][n][r], sc[m], n) >= tau[n]) ? (1u << r) : 0u;
+                            while (mask) {
+                                const int r = __builtin_ctz(mask);
+                                mask &= mask - 1;
+                                const uint32_t row = rbase + (r & 3) + 8 * (r >> 2);
+                                if (row >= p.n_rows) continue;
+                                auto av = acc[m][n][0];
+#pragma unroll
+                                for (int rr = 1; rr < 16; ++rr) av = (rr == r) ? acc[m][n][rr] : av;
+                                const float v = score(av, sc[m], n);
+                                uint32_t pos;
+                                asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                                             : "=v"(pos) : "v"(ecnt_addr), "v"(1u) : "memory");
+                                if (pos < (uint32_t)(kWCap - 1)) {
+                                    ekeys[pos] = score_key(v, row);
+                                    eq[pos] = ql;
+                                } else {  // wave buffer full: straight to the global list
+                                    const uint32_t q = qt * BN + ql;
+                                    const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                                    if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v, row);
+                                    stored = true;
+                                }
+                            }
+                            stored = __ballot(stored) != 0;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+                }
+            }
+            // global stores / atomics count in vmcnt: drain them so the counted waits stay exact
+            if (stored) wait_vm0();
+            kt = 0;
+            ++ti;
+        } else {
+            ++kt;
+        }
+    }
+    if constexpr (EMIT) {
+        const uint32_t ecount = eq[kWCap - 1];
+        const uint32_t ne = ecount < (uint32_t)(kWCap - 1) ? ecount : (uint32_t)(kWCap - 1);
+        for (uint32_t i = lane; i < ne; i += kWave) {
+            const uint32_t q = qt * BN + eq[i];
+            const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+            if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Threshold per query from the sample scores: tau0 = the ks-th largest value of S (sample
+// scores, or their maxima over 32 sampled rows -- never above the ks-th largest sample),
+// so that about ks * stride rows of the shard or more reach it.  4 waves per query.  Also
+// zeroes the query's candidate counter and (block 0) the emit status words.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S, uint32_t s_ld,
+                                                    uint32_t n_s, uint32_t nq, uint32_t qpad,
+                                                    const uint32_t* __restrict__ qflags,
+                                                    uint32_t ks, float* __restrict__ tau,
+                                                    uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ status) {
+    __shared__ uint64_t part[4][64];
+    const uint32_t q = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; }
+    if (q >= qpad) return;
+    if (t == 0) cnt[q] = 0;
+    if (q >= nq || (qflags[q] & kQueryNoApprox)) {
+        if (t == 0) tau[q] = INFINITY;  // never emits: answered by the exact scan
+        return;
+    }
+    if (n_s < ks) {
+        if (t == 0) tau[q] = -INFINITY;
+        return;
+    }
+    // wave w streams a quarter of the values, keeping its ks best
+    WaveTopK<1> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    const float* s = S + (uint64_t)q * s_ld;
+    const uint32_t per = (n_s + 3) / 4, lo = w * per, hi = lo + per < n_s ? lo + per : n_s;
+    for (uint32_t base = lo; base < hi; base += kWave) {
+        const uint32_t i = base + lane;
+        L.offer(i < hi ? score_key(s[i], i) : kKeyNone, (int)ks, thr);
+    }
+    part[w][lane] = L.v[0];
+    __syncthreads();
+    if (w == 0) {
+        WaveTopK<1> M;
+        M.init();
+        uint64_t mt = kKeyNone;
+        for (int src = 0; src < 4; ++src) M.offer(part[src][lane], (int)ks, mt);
+        if (lane == 0) tau[q] = score_key_score(mt);
+    }
+}
+
+// Top-(kp+1) of the emitted candidates by (score desc, row asc); the first kp go to the
+// exact rescore, the (kp+1)-th score bounds every row left out.  One wave per query.
+template <int E>
+__global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__ cand,
+                                                    const uint32_t* __restrict__ cnt, uint32_t cap,
+                                                    uint32_t nq, const float* __restrict__ tau,
+                                                    uint32_t kp, uint32_t* __restrict__ cand_rows,
+                                                    uint32_t* __restrict__ ncand,
+                                                    float* __restrict__ tau_excl,
+                                                    uint32_t* __restrict__ status) {
+    const uint32_t q = blockIdx.x;
+    if (q >= nq) return;
+    const uint32_t c = cnt[q];
+    if (threadIdx.x == 0) atomicAdd(status + kStEmitted, c);
+    if (c > cap) {  // overflow: rows were dropped, nothing can be certified
+        if (threadIdx.x == 0) { ncand[q] = 0; tau_excl[q] = INFINITY; }
+        return;
+    }
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    const uint64_t* src = cand + (uint64_t)q * cap;
+    for (uint32_t base = 0; base < c; base += kWave) {
+        const uint32_t i = base + threadIdx.x;
+        L.offer(i < c ? src[i] : kKeyNone, (int)kp + 1, thr);
+    }
+    const uint32_t nc = c < kp ? c : kp;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t pidx = e * kWave + threadIdx.x;
+        if (pidx < nc) cand_rows[(uint64_t)q * kp + pidx] = key_row(L.v[e]);
+    }
+    if (threadIdx.x == 0) {
+        ncand[q] = nc;
+        tau_excl[q] = c > kp ? score_key_score(thr) : tau[q];
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------
+// Workgroups for the persistent filter: 8 XCDs x (32 CUs rounded down to a multiple of n_qt).
+static uint32_t filter_grid(uint32_t n_qt) {
+    const uint32_t per_xcd = n_qt >= 32 ? n_qt : (32 / n_qt) * n_qt;
+    return 8 * per_xcd;
+}
+
+hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s) {
+    if (op == kFilterI8)
+        hipLaunchKernelGGL((k_filter<OpI8, false>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_filter<OpBF16, false>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s) {
+    if (op == kFilterI8)
+        hipLaunchKernelGGL((k_filter<OpI8, true>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_filter<OpBF16, true>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,
+                             const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(k_select_tau, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau, cnt,
+                       status);
+    return hipGetLastError();
+}
+hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,
+                              const float* tau, uint32_t kp, uint32_t* cand_rows, uint32_t* ncand,
+                              float* tau_excl, uint32_t* status, hipStream_t s) {
+    const uint32_t e = (kp + 1 + 63) / 64;
+#define BSR_SELECT(E)                                                                                   \
+    hipLaunchKernelGGL(k_select_cand<E>, dim3(nq), dim3(64), 0, s, cand, cnt, cap, nq, tau, kp, cand_rows, \
+                       ncand, tau_excl, status)
+    switch (e) {
+        case 1: BSR_SELECT(1); break;
+        case 2: BSR_SELECT(2); break;
+        case 3: BSR_SELECT(3); break;
+        case 4: BSR_SELECT(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef BSR_SELECT
+    return hipGetLastError();
+}
+
+}  // namespace bsr

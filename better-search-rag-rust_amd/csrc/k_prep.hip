@@ -1,0 +1,401 @@
+// k_prep.hip -- data movement and preparation kernels (gfx950): synthetic data, the padded
+// f32 slab, the reference's exact magnitudes, and the MFMA filter operands (bf16 or int8)
+// of corpus rows and queries together with their certification error bounds.
+//
+// Compiled with -ffp-contract=off: the magnitudes reproduce src/metrics.rs:154-155 (a
+// sequential f32 sum of squares in index order, then a correctly rounded sqrt).  The
+// filter operands are approximations whose error is measured here, in double precision,
+// and carried to the certification step.
+#include "bsr_device.hpp"
+#include "kernels.hpp"
+
+#include <math.h>
+
+namespace bsr {
+
+// ------------------------------------------------------------------------------------
+// Synthetic data: value(row, col) = U[-1,1) from splitmix64(seed, row*dim + col), 24 bits.
+// ------------------------------------------------------------------------------------
+__global__ void k_synth_uniform(float* __restrict__ out, uint64_t row0, uint64_t n_rows,
+                                uint32_t dim, uint32_t ld, uint64_t seed) {
+    const uint64_t total = n_rows * (uint64_t)ld;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = e / ld;
+        const uint32_t c = (uint32_t)(e - r * ld);
+        float v = 0.0f;
+        if (c < dim) {
+            const uint64_t g = (row0 + r) * (uint64_t)dim + c;
+            const uint64_t h = splitmix64(seed * 0xD1B54A32D192ED03ull + g);
+            v = (float)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;  // 24-bit grid on [-1, 1)
+        }
+        out[e] = v;
+    }
+}
+
+// Dense copy into the padded [n][ld] layout (zeros in the pad columns).
+__global__ void k_copy_rows_f32(const float* __restrict__ src, uint64_t n, uint32_t dim,
+                                uint32_t ld, float* __restrict__ dst) {
+    const uint64_t total = n * (uint64_t)ld;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = e / ld;
+        const uint32_t c = (uint32_t)(e - r * ld);
+        dst[e] = c < dim ? src[r * dim + c] : 0.0f;
+    }
+}
+
+__global__ void k_widen_bf16_rows(const uint16_t* __restrict__ src, uint64_t n, uint32_t dim,
+                                  uint32_t ld, float* __restrict__ dst) {
+    const uint64_t total = n * (uint64_t)ld;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = e / ld;
+        const uint32_t c = (uint32_t)(e - r * ld);
+        dst[e] = c < dim ? bf16_to_f32(src[r * dim + c]) : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Row magnitudes exactly as src/metrics.rs:154: sqrt of the sequential f32 sum of a_i*a_i.
+// One lane per row; the per-row dependency chain is inherently serial.
+// ------------------------------------------------------------------------------------
+__global__ void k_row_norms(const float* __restrict__ rows, uint64_t n, uint32_t dim,
+                            uint32_t ld, float* __restrict__ na, uint32_t* flags) {
+    const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint32_t f = 0;
+    if (r < n) {
+        const float* a = rows + r * ld;
+        float acc = -0.0f;
+        bool bad = false;
+        uint32_t i = 0;
+        for (; i + 4 <= dim; i += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(a + i);
+            bad = bad || !isfinite(x.x) || !isfinite(x.y) || !isfinite(x.z) || !isfinite(x.w);
+            acc = acc + x.x * x.x;
+            acc = acc + x.y * x.y;
+            acc = acc + x.z * x.z;
+            acc = acc + x.w * x.w;
+        }
+        for (; i < dim; ++i) {
+            const float x = a[i];
+            bad |= !isfinite(x);
+            acc = acc + x * x;
+        }
+        const float m = __builtin_sqrtf(acc);
+        na[r] = m;
+        if (bad) f |= kRowNonFinite;
+        if (!isfinite(m)) f |= kRowNormOvf;
+        if (m != 0.0f && (m < 1e-18f || m > 1e18f)) f |= kRowNormRange;
+    }
+    const uint32_t any = __reduce_or_sync(~0ull, f);
+    if (any && lane_id() == 0) atomicOr(flags, any);
+}
+
+// Normalised bf16 copy for the bf16 filter: bf16_rne(a_i / |a|), zero rows / pad -> 0.
+// Each thread writes 8 consecutive elements (16 B).
+__global__ void k_rows_to_bf16n(const float* __restrict__ rows, const float* __restrict__ na,
+                                uint64_t n, uint64_t n_pad, uint32_t dim, uint32_t ld,
+                                uint16_t* __restrict__ out) {
+    const uint64_t groups = n_pad * (uint64_t)(ld / 8);
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = g / (ld / 8);
+        const uint32_t c0 = (uint32_t)(g - r * (ld / 8)) * 8;
+        uint16_t h[8];
+        const float m = r < n ? na[r] : 0.0f;
+        const bool ok = r < n && m != 0.0f && isfinite(m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t c = c0 + j;
+            h[j] = (ok && c < dim) ? f32_to_bf16_rne(rows[r * ld + c] / m) : (uint16_t)0;
+        }
+        uint4 v;
+        v.x = h[0] | ((uint32_t)h[1] << 16);
+        v.y = h[2] | ((uint32_t)h[3] << 16);
+        v.z = h[4] | ((uint32_t)h[5] << 16);
+        v.w = h[6] | ((uint32_t)h[7] << 16);
+        *reinterpret_cast<uint4*>(out + r * ld + c0) = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// int8 filter operand.  One workgroup (4 waves) per block of 32 rows, the rows of one
+// 32x32 MFMA accumulator block:
+//   x = a / |a|                      (double; |a| = sqrt of the double sum of squares)
+//   s = the smallest f32 >= max_block |x_i| / 127
+//   q_i = rint(x_i / s) in [-127, 127]
+//   e_row = || x - s q ||_2          (double), ea_max = max_row e_row rounded up to f32.
+// By Cauchy-Schwarz |x.y - (s q).(t p)| <= e_row + e_q + e_row e_q for unit x, y, which is
+// the row-side half of the certification bound.  Zero rows give q = 0 and e = 0 (the
+// reference scores them 1.0 = cosine 0, which is exactly the filter's value).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+// Smallest f32 >= x (x >= 0, finite).
+__device__ __forceinline__ float f32_round_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+__device__ __forceinline__ int8_t quant_i8(double x, double s) {
+    double qd = rint(x / s);
+    qd = fmin(127.0, fmax(-127.0, qd));
+    return (int8_t)(int)qd;
+}
+
+__global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ rows, uint64_t n,
+                                                    uint32_t dim, uint32_t ld,
+                                                    int8_t* __restrict__ out,
+                                                    float* __restrict__ scales,
+                                                    uint32_t* __restrict__ ea_max) {
+    __shared__ double s_inv[kQuantBlock];
+    __shared__ double s_wmax[4];
+    const uint64_t blk = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    constexpr int kRowsPerWave = kQuantBlock / 4;
+    double wmax = 0.0;
+    for (int i = 0; i < kRowsPerWave; ++i) {
+        const int rl = w * kRowsPerWave + i;
+        const uint64_t r = blk * kQuantBlock + rl;
+        double ss = 0.0, mx = 0.0;
+        if (r < n) {
+            const float* a = rows + r * ld;
+            for (uint32_t c = lane; c < dim; c += kWave) {
+                const double x = a[c];
+                ss += x * x;
+                mx = fmax(mx, fabs(x));
+            }
+        }
+        ss = wave_sum_f64(ss);
+        mx = wave_max_f64(mx);
+        const double inv = (ss > 0.0 && ss < 1e300) ? 1.0 / sqrt(ss) : 0.0;
+        if (lane == 0) s_inv[rl] = inv;
+        wmax = fmax(wmax, mx * inv);
+    }
+    if (lane == 0) s_wmax[w] = wmax;
+    __syncthreads();
+    const double bmax = fmax(fmax(s_wmax[0], s_wmax[1]), fmax(s_wmax[2], s_wmax[3]));
+    const float sc = bmax > 0.0 ? f32_round_up(bmax / 127.0) : 1.0f;
+    if (t == 0) scales[blk] = sc;
+    const double s = sc;
+    double ew = 0.0;
+    for (int i = 0; i < kRowsPerWave; ++i) {
+        const int rl = w * kRowsPerWave + i;
+        const uint64_t r = blk * kQuantBlock + rl;
+        const double inv = s_inv[rl];
+        const float* a = rows + r * ld;
+        double e2 = 0.0;
+        for (uint32_t c0 = lane * 4; c0 < ld; c0 += 4 * kWave) {
+            char4 v = make_char4(0, 0, 0, 0);
+            int8_t qv[4] = {0, 0, 0, 0};
+            if (r < n && inv > 0.0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t c = c0 + j;
+                    if (c < dim) {
+                        const double x = (double)a[c] * inv;
+                        qv[j] = quant_i8(x, s);
+                        const double d = x - s * (double)qv[j];
+                        e2 += d * d;
+                    }
+                }
+            }
+            v.x = qv[0]; v.y = qv[1]; v.z = qv[2]; v.w = qv[3];
+            *reinterpret_cast<char4*>(out + r * ld + c0) = v;
+        }
+        e2 = wave_sum_f64(e2);
+        ew = fmax(ew, sqrt(e2));
+    }
+    if (lane == 0) atomicMax(ea_max, __float_as_uint(f32_round_up(ew * (1.0 + 1e-9) + 1e-12)));
+}
+
+// ------------------------------------------------------------------------------------
+// Queries.
+// k_query_norms: 64 queries per wave, 64-column chunks staged through LDS (coalesced reads),
+// each lane then walks its own query in index order: |b| exactly as src/metrics.rs:155,
+// finiteness and eligibility for the filter.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_query_norms(const float* __restrict__ q, uint32_t nq, uint32_t qpad,
+                                                    uint32_t dim, FilterOp op, float* __restrict__ nb,
+                                                    float* __restrict__ ebound,
+                                                    uint32_t* __restrict__ qflags,
+                                                    uint32_t* __restrict__ status) {
+    __shared__ float tile[64][65];
+    const int lane = threadIdx.x;
+    const uint32_t q0 = blockIdx.x * 64, qi = q0 + lane;
+    float acc = -0.0f;
+    bool bad = false;
+    for (uint32_t c0 = 0; c0 < dim; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        for (int r = 0; r < 64; ++r) {
+            const uint32_t qq = q0 + r;
+            tile[r][lane] = (qq < nq && c < dim) ? q[(uint64_t)qq * dim + c] : 0.0f;
+        }
+        __syncthreads();
+        const uint32_t nv = dim - c0 < 64 ? dim - c0 : 64;
+        for (uint32_t i = 0; i < nv; ++i) {
+            const float x = tile[lane][i];
+            bad = bad || !isfinite(x);
+            acc = acc + x * x;
+        }
+        __syncthreads();
+    }
+    if (qi >= qpad) return;
+    if (qi >= nq) {
+        nb[qi] = 0.0f;
+        qflags[qi] = kQueryNoApprox;
+        ebound[qi] = INFINITY;
+        return;
+    }
+    const float m = __builtin_sqrtf(acc);
+    nb[qi] = m;
+    const bool approx_ok = !bad && isfinite(m) && m >= 1e-18f && m <= 1e18f;
+    const uint32_t f = (bad ? kQueryNonFinite : 0u) | (approx_ok ? 0u : kQueryNoApprox);
+    qflags[qi] = f;
+    // bf16: the constant bound; i8: written by k_query_i8
+    if (op == kFilterBF16) ebound[qi] = approx_ok ? (float)kEBoundBF16 : INFINITY;
+    if (f & kQueryNonFinite) atomicOr(status + kStQueryFlags, kQueryNonFinite);
+}
+
+// Padded f32 copy [qpad][ld] and, for the bf16 filter, the normalised bf16 copy.
+__global__ void k_query_convert(const float* __restrict__ q, uint32_t nq, uint32_t qpad, uint32_t dim,
+                                uint32_t ld, const float* __restrict__ nb,
+                                const uint32_t* __restrict__ qflags, float* __restrict__ qf32,
+                                uint16_t* __restrict__ qbf) {
+    const uint64_t total = (uint64_t)qpad * ld;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t qi = (uint32_t)(e / ld), c = (uint32_t)(e - (uint64_t)qi * ld);
+        const float v = (qi < nq && c < dim) ? q[(uint64_t)qi * dim + c] : 0.0f;
+        qf32[e] = v;
+        if (qbf) {
+            const bool ok = qi < nq && c < dim && !(qflags[qi] & kQueryNoApprox);
+            qbf[e] = ok ? f32_to_bf16_rne(v / nb[qi]) : (uint16_t)0;
+        }
+    }
+}
+
+// int8 query operand, one wave per query (same construction as k_rows_to_i8 with a
+// per-query scale), and the per-query certification bound
+//   E_q = ea + eb + ea*eb + 1.5e-4
+// (ea: row side, eb: this query; 1.5e-4 covers the reference's own f32 rounding, <= 9.3e-5,
+// and the two f32 roundings of the filter's score).
+__global__ __launch_bounds__(64) void k_query_i8(const float* __restrict__ qf32, uint32_t nq, uint32_t dim,
+                                                 uint32_t ld, const uint32_t* __restrict__ qflags,
+                                                 const uint32_t* __restrict__ ea_max,
+                                                 int8_t* __restrict__ qi8, float* __restrict__ qscale,
+                                                 float* __restrict__ ebound) {
+    const uint32_t qi = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float* b = qf32 + (uint64_t)qi * ld;
+    int8_t* o = qi8 + (uint64_t)qi * ld;
+    const bool ok = qi < nq && !(qflags[qi] & kQueryNoApprox);
+    double ss = 0.0, mx = 0.0;
+    if (ok) {
+        for (uint32_t c = lane; c < dim; c += kWave) {
+            const double x = b[c];
+            ss += x * x;
+            mx = fmax(mx, fabs(x));
+        }
+    }
+    ss = wave_sum_f64(ss);
+    mx = wave_max_f64(mx);
+    const double inv = ok && ss > 0.0 ? 1.0 / sqrt(ss) : 0.0;
+    const float sc = (ok && mx > 0.0) ? f32_round_up(mx * inv / 127.0) : 1.0f;
+    const double s = sc;
+    double e2 = 0.0;
+    for (uint32_t c0 = lane * 4; c0 < ld; c0 += 4 * kWave) {
+        int8_t qv[4] = {0, 0, 0, 0};
+        if (ok) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t c = c0 + j;
+                if (c < dim) {
+                    const double x = (double)b[c] * inv;
+                    qv[j] = quant_i8(x, s);
+                    const double d = x - s * (double)qv[j];
+                    e2 += d * d;
+                }
+            }
+        }
+        *reinterpret_cast<char4*>(o + c0) = make_char4(qv[0], qv[1], qv[2], qv[3]);
+    }
+    e2 = wave_sum_f64(e2);
+    if (lane == 0) {
+        qscale[qi] = ok ? sc : 0.0f;
+        if (ok) {
+            const double ea = (double)__uint_as_float(*ea_max);
+            const double eb = sqrt(e2) * (1.0 + 1e-9) + 1e-12;
+            ebound[qi] = f32_round_up(ea + eb + ea * eb + 1.5e-4);
+        } else {
+            ebound[qi] = INFINITY;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------
+static inline uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap = 65536) {
+    uint64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    return (uint32_t)(g > cap ? cap : g);
+}
+
+hipError_t launch_synth_uniform(float* out, uint64_t row0, uint64_t n_rows, uint32_t dim,
+                                uint32_t ld, uint64_t seed, hipStream_t s) {
+    hipLaunchKernelGGL(k_synth_uniform, dim3(grid_for(n_rows * ld, 256)), dim3(256), 0, s, out, row0,
+                       n_rows, dim, ld, seed);
+    return hipGetLastError();
+}
+hipError_t launch_copy_rows_f32(const float* src, uint64_t n, uint32_t dim, uint32_t ld, float* dst,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_copy_rows_f32, dim3(grid_for(n * ld, 256)), dim3(256), 0, s, src, n, dim, ld, dst);
+    return hipGetLastError();
+}
+hipError_t launch_widen_bf16_rows(const uint16_t* src, uint64_t n, uint32_t dim, uint32_t ld,
+                                  float* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_widen_bf16_rows, dim3(grid_for(n * ld, 256)), dim3(256), 0, s, src, n, dim, ld, dst);
+    return hipGetLastError();
+}
+hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t dim, uint32_t ld, float* na,
+                            uint32_t* flags, hipStream_t s) {
+    hipLaunchKernelGGL(k_row_norms, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, rows, n, dim, ld,
+                       na, flags);
+    return hipGetLastError();
+}
+hipError_t launch_rows_to_bf16n(const float* rows, const float* na, uint64_t n, uint64_t n_pad,
+                                uint32_t dim, uint32_t ld, uint16_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_rows_to_bf16n, dim3(grid_for(n_pad * (ld / 8), 256)), dim3(256), 0, s, rows, na, n,
+                       n_pad, dim, ld, out);
+    return hipGetLastError();
+}
+hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint32_t dim, uint32_t ld,
+                             int8_t* out, float* scales, uint32_t* ea_max, hipStream_t s) {
+    const uint64_t blocks = n_pad / kQuantBlock;
+    hipLaunchKernelGGL(k_rows_to_i8, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, dim, ld, out, scales,
+                       ea_max);
+    return hipGetLastError();
+}
+hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_query_norms, dim3((a.qpad + 63) / 64), dim3(64), 0, s, a.q, a.nq, a.qpad, a.dim, a.op,
+                       a.nb, a.ebound, a.qflags, a.status);
+    hipLaunchKernelGGL(k_query_convert, dim3(grid_for((uint64_t)a.qpad * a.ld, 256)), dim3(256), 0, s, a.q, a.nq,
+                       a.qpad, a.dim, a.ld, a.nb, a.qflags, a.qf32,
+                       a.op == kFilterBF16 ? static_cast<uint16_t*>(a.qop) : nullptr);
+    if (a.op == kFilterI8)
+        hipLaunchKernelGGL(k_query_i8, dim3(a.qpad), dim3(64), 0, s, a.qf32, a.nq, a.dim, a.ld, a.qflags, a.ea_max,
+                           static_cast<int8_t*>(a.qop), a.qscale, a.ebound);
+    return hipGetLastError();
+}
+
+}  // namespace bsr

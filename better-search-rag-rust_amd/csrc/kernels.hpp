@@ -1,4 +1,5 @@
-// kernels.hpp -- host-side launchers for the gfx950 kernels in kernels.hip.
+// kernels.hpp -- host-side launchers for the gfx950 kernels (k_prep.hip, k_filter.hip,
+// k_exact.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -7,12 +8,18 @@
 namespace bsr {
 
 // Layout constants shared by the host orchestration and the kernels.
-constexpr uint32_t kLdAlign = 64;      // f32/bf16 row leading dimension multiple (elements)
+constexpr uint32_t kLdAlign = 64;      // f32 row leading dimension multiple (elements)
 constexpr uint32_t kRowPad = 256;      // rows are padded to a multiple of this (zero rows)
-constexpr uint32_t kGemmBM = 128;      // MFMA filter tile: corpus rows
-constexpr uint32_t kGemmBN = 128;      // MFMA filter tile: queries
 constexpr uint32_t kScanQF = 8;        // queries per exact-scan launch (max)
 constexpr uint32_t kSampleStride = 32; // candidate-threshold sample: every 32nd row
+constexpr uint32_t kQuantBlock = 32;   // rows sharing one int8 scale (one 32-row MFMA block)
+constexpr uint32_t kFilterTile = 256;  // MFMA filter tile: 256 corpus rows x 256 queries
+
+// Operand type of the MFMA candidate filter.
+enum FilterOp : uint32_t {
+    kFilterI8 = 0,    // int8 rows/queries, per-32-row-block and per-query scales, i32 MFMA
+    kFilterBF16 = 1,  // bf16(a/|a|), bf16(b/|b|), f32-accumulating bf16 MFMA
+};
 
 // Row-state flags (index load).
 constexpr uint32_t kRowNonFinite = 1u;  // a NaN/Inf element
@@ -23,6 +30,13 @@ constexpr uint32_t kRowNormRange = 4u;  // nonzero norm outside [1e-18, 1e18]: n
 constexpr uint32_t kQueryNonFinite = 1u;
 constexpr uint32_t kQueryNoApprox = 2u;   // norm zero/tiny/huge: answered by the exact scan
 
+// Search status words (device, one small D2H copy per search).
+enum StatusWord : uint32_t { kStFail = 0, kStEmitted = 1, kStQueryFlags = 2, kStWords = 4 };
+
+// Certification bound of the bf16 filter.
+constexpr double kEBoundBF16 = 8.5e-3;
+
+// ---- data movement / load-time preparation (k_prep.hip) -------------------------------
 hipError_t launch_synth_uniform(float* out, uint64_t row0, uint64_t n_rows, uint32_t dim,
                                 uint32_t ld, uint64_t seed, hipStream_t s);
 hipError_t launch_copy_rows_f32(const float* src, uint64_t n, uint32_t dim, uint32_t ld,
@@ -33,45 +47,70 @@ hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t dim, uint32_
                             float* na, uint32_t* flags, hipStream_t s);
 hipError_t launch_rows_to_bf16n(const float* rows, const float* na, uint64_t n, uint64_t n_pad,
                                 uint32_t dim, uint32_t ld, uint16_t* out, hipStream_t s);
-hipError_t launch_query_prep(const float* q, uint32_t nq, uint32_t qpad, uint32_t dim,
-                             uint32_t ld, float* qf32, float* nb, uint16_t* qbf,
-                             uint32_t* qflags, hipStream_t s);
+// int8 filter operand: per 32-row block scale s (127*s >= max |a_i|/|a| over the block),
+// q_i = rint(a_i/(|a| s)); ea_max (u32 bits of a non-negative float, atomicMax) receives
+// an upper bound of max_row || a/|a| - s q ||_2.
+hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint32_t dim,
+                             uint32_t ld, int8_t* out, float* scales, uint32_t* ea_max,
+                             hipStream_t s);
+// Query preparation: exact |b| (src/metrics.rs:155), flags, padded f32 copy, the filter
+// operand (bf16 or int8 + scale) and the per-query certification bound ebound[q].
+struct QueryPrepArgs {
+    const float* q;        // caller's queries [nq][dim]
+    uint32_t nq, qpad, dim, ld;
+    FilterOp op;
+    const uint32_t* ea_max;  // i8: row-side error bound (device word)
+    float* qf32;           // [qpad][ld]
+    float* nb;             // [qpad]
+    void* qop;             // bf16 [qpad][ld] or int8 [qpad][ld]
+    float* qscale;         // i8: [qpad]
+    float* ebound;         // [qpad]
+    uint32_t* qflags;      // [qpad]
+    uint32_t* status;      // kStQueryFlags word receives the OR of the flags
+};
+hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s);
 
+// ---- MFMA candidate filter (k_filter.hip) ---------------------------------------------
 struct GemmArgs {
-    const uint16_t* A;      // normalised bf16 corpus [n_pad][ld]
-    uint64_t a_row_stride;  // elements between consecutive tile rows (ld or ld*sample stride)
+    const uint8_t* A;       // filter rows [n_pad][row_bytes]
+    uint64_t a_stride;      // bytes between consecutive tile rows (row_bytes, or x sample stride)
     uint32_t n_rows;        // valid tile rows (n for emit, n_sample for the sample pass)
-    const uint16_t* B;      // normalised bf16 queries [qpad][ld]
-    uint32_t ld;
+    uint32_t a_row_mult;    // corpus row of tile row r = r * a_row_mult (1 emit, 32 sample)
+    const uint8_t* B;       // filter queries [qpad][row_bytes]
+    uint32_t row_bytes;     // bytes of one operand row (multiple of 64)
     uint32_t n_rt, n_qt;    // row tiles, query tiles
+    const float* a_scale;   // i8: [n_pad / 32] block scales
+    const float* b_scale;   // i8: [qpad] query scales
     float* S;               // sample: scores [qpad][s_ld]
     uint32_t s_ld;
+    uint32_t s_compact;     // sample: 1 = one maximum per 32 sampled rows, 0 = every score
     const float* tau;       // emit: per-query threshold
     uint64_t* cand;         // emit: [qpad][cap] score keys
     uint32_t* cnt;          // emit: [qpad] counters
     uint32_t cap;
 };
-// Tile geometry of the active filter kernel (BSR_GEMM_VARIANT=1 selects the v1 128x128
-// kernel for A/B comparisons; default v2 = persistent 256x256).
-uint32_t gemm_query_pad();
-uint32_t gemm_row_tile();
-hipError_t launch_gemm_sample(const GemmArgs& a, hipStream_t s);
-hipError_t launch_gemm_emit(const GemmArgs& a, hipStream_t s);
+hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s);
+hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s);
 
+// tau[q] = the ks-th best sampled score; also zeroes cnt[0..qpad) and the status words
+// kStFail / kStEmitted for the emit pass that follows.
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq,
                              uint32_t qpad, const uint32_t* qflags, uint32_t ks, float* tau,
-                             hipStream_t s);
+                             uint32_t* cnt, uint32_t* status, hipStream_t s);
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap,
                               uint32_t nq, const float* tau, uint32_t kp, uint32_t* cand_rows,
-                              uint32_t* ncand, float* tau_excl, hipStream_t s);
+                              uint32_t* ncand, float* tau_excl, uint32_t* status,
+                              hipStream_t s);
+
+// ---- exact arithmetic (k_exact.hip) ---------------------------------------------------
 hipError_t launch_rescore(const float* rows, uint32_t ld, uint32_t dim, const float* na,
                           const float* qf32, const float* nb, uint32_t nq,
                           const uint32_t* cand_rows, const uint32_t* ncand, uint32_t kp,
-                          const float* tau_excl, uint32_t k, double ebound,
-                          uint64_t* out_keys, uint32_t* fail_cnt, uint32_t* fail_list,
+                          const float* tau_excl, uint32_t k, const float* ebound,
+                          uint64_t* out_keys, uint32_t* status, uint32_t* fail_list,
                           hipStream_t s);
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold
-// grid * kScanQF * k keys; returns the grid used through *grid_out.
+// grid * kScanQF * k keys.
 hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint64_t n,
                              const float* na, const float* qf32, const int32_t* qids,
                              uint32_t nqf, const float* nb, uint32_t k, uint32_t grid,
@@ -83,7 +122,6 @@ hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64
                            uint32_t* out_count, hipStream_t s);
 hipError_t launch_cosine_pair(const float* a, uint32_t la, const float* b, uint32_t lb,
                               float* out, hipStream_t s);
-hipError_t launch_check_finite(const float* x, uint64_t count, uint32_t* flag, hipStream_t s);
 
 uint32_t scan_grid_for(uint64_t n);
 

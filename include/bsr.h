@@ -63,6 +63,11 @@ typedef struct {
 #define BSR_MAX_K 256u
 #define BSR_FLAG_EXACT_ONLY 1u /* never use the MFMA candidate stage (always full exact scan) */
 #define BSR_FLAG_PROFILE 2u    /* record per-kernel HIP events (bsr_index_profile) */
+/* MFMA candidate filter operand: int8 (default; v_mfma_i32_32x32x32_i8, per-32-row-block
+ * and per-query scales, certified with a measured Cauchy-Schwarz bound) or bf16 with this
+ * flag (v_mfma_f32_32x32x16_bf16, certified with a constant bound).  Either way every
+ * returned list is exact; the filter only decides how much exact work a query needs. */
+#define BSR_FLAG_FILTER_BF16 4u
 
 /* Mirrors RankInterval {start_index, end_index} (load_balance.rs:8-17). end < start means
  * an empty block, as in the reference's release build. */
@@ -81,6 +86,8 @@ typedef struct {
     uint32_t n_fallback;       /* queries whose MFMA candidate set failed certification */
     uint32_t n_candidates;     /* k' candidates rescored per query */
     uint64_t n_emitted;        /* candidates emitted by the MFMA filter (all queries) */
+    uint32_t filter_op;        /* 0 = int8 filter, 1 = bf16 filter (BSR_FLAG_FILTER_BF16) */
+    float row_ebound;          /* int8: max over rows of ||a/|a| - s q||_2 (0 for bf16) */
 } bsr_search_stats;
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts

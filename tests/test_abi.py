@@ -35,7 +35,7 @@ def test_library_is_native_gfx950(bsr_mod):
     # the .so carries a gfx950 code object (kernels are compiled for MI355X, not a fallback)
     blob = open(bsr_mod.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
-    assert b"k_gemm_filter" in blob and b"k_scan_exact" in blob
+    assert b"k_filter" in blob and b"k_scan_exact" in blob
 
 
 def test_interval_matches_known_and_oracle(bsr_mod, oracle_mod):

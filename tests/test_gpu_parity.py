@@ -96,14 +96,20 @@ def test_exact_scan_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
 
 
+FILTERS = pytest.mark.parametrize("fflags", [0, 4], ids=["i8", "bf16"])  # 4 = BSR_FLAG_FILTER_BF16
+
+
+@FILTERS
 @pytest.mark.parametrize("n,dim,nq,k", [
     (20000, 768, 32, 10),   # config 1 stand-in (JabRef ~20k chunks, 32 queries, top-10)
     (20000, 768, 40, 50),   # the reference's own k = 50 (src/main.rs:110)
     (30000, 256, 20, 100),
     (2500, 768, 64, 10),    # n <= candidate cap: no sample pass, tau = -inf
     (50000, 96, 17, 200),
+    (100000, 768, 24, 10),  # large shard: compact sample (maxima over 32 sampled rows)
+    (5000, 40, 16, 10),     # 64-byte int8 rows: one K slice per tile
 ])
-def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
+def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
     rng = np.random.default_rng(7 * n + k)
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
     rows[n - 1] = rows[0]            # duplicate pair far apart
@@ -112,23 +118,43 @@ def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
     qs[0] = rows[0]
     qs[1] = rows[20]
-    ix = _index(bsr_mod, rows)
+    ix = _index(bsr_mod, rows, flags=fflags)
     got = ix.local_top_k(qs, k)
     st = ix.last_stats()
     assert st.n_exact_direct == 0 and st.n_candidates >= k
+    assert st.filter_op == (1 if fflags else 0)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
     # both copies of row 0 lead query 0's list at distance 0, smaller index first
     assert list(got[0][0, :2]) == [0, n - 1] and got[1][0, 0] == 0 and got[1][0, 1] == 0
 
 
-def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu):
+@FILTERS
+def test_filter_certifies_uniform_data(bsr_mod, oracle_mod, gpu, fflags):
+    # Independent U(-1,1) queries over a U(-1,1) corpus (the bench's data): the filter must
+    # certify every query (a broken filter would still be exact, through fallbacks).
+    rng = np.random.default_rng(11)
+    rows = rng.uniform(-1, 1, (60000, 768)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (48, 768)).astype(np.float32)
+    qs[0] = rows[123]
+    ix = _index(bsr_mod, rows, flags=fflags)
+    got = ix.local_top_k(qs, 10)
+    st = ix.last_stats()
+    assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
+    assert st.n_emitted >= 48 * 64
+    if not fflags:
+        assert 1e-3 < st.row_ebound < 6e-3, st.row_ebound
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "uniform")
+
+
+@FILTERS
+def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu, fflags):
     # Clustered embeddings (dense neighbourhoods) stress the certification; any query it
     # cannot certify must fall back to the exact scan and still be exact.
     rng = np.random.default_rng(42)
     centers = rng.normal(size=(20, 768)).astype(np.float32)
     rows = (centers[rng.integers(0, 20, 40000)] + 0.05 * rng.normal(size=(40000, 768))).astype(np.float32)
     qs = (centers[rng.integers(0, 20, 24)] + 0.05 * rng.normal(size=(24, 768))).astype(np.float32)
-    ix = _index(bsr_mod, rows)
+    ix = _index(bsr_mod, rows, flags=fflags)
     got = ix.local_top_k(qs, 10)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "clusters")
 

@@ -1,7 +1,8 @@
-// Microbenchmark (tooling): the MFMA filter kernel and its ablations on a synthetic shard.
-// Includes the product kernels directly.  Build:
+// Microbenchmark (tooling): the MFMA filter kernel (int8 and bf16 operands) and its
+// ablations on a synthetic shard.  Includes the product kernel source directly.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../../include -I../../better-search-rag-rust_amd/csrc gemm_ablate.hip -o gemm_ablate
-#include "kernels.hip"
+// Run: ./gemm_ablate [rows] [queries] [rounds]
+#include "k_filter.hip"
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
@@ -9,6 +10,7 @@
 using namespace bsr;
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
+// bf16: U(-0.036, 0.036) per element; int8: U{-127..127} (scores = I * s_a * s_b)
 __global__ void fill_bf16(uint16_t* p, size_t n, uint64_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t h = splitmix64(seed + i);
@@ -16,52 +18,55 @@ __global__ void fill_bf16(uint16_t* p, size_t n, uint64_t seed) {
         p[i] = f32_to_bf16_rne(v);
     }
 }
-
-template <class F>
-float timeit(F f, int reps = 5) {
-    hipEvent_t a, b;
-    CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
-    f(); CHECK(hipDeviceSynchronize());
-    float best = 1e30f;
-    for (int r = 0; r < reps; ++r) {
-        CHECK(hipEventRecord(a)); f(); CHECK(hipEventRecord(b)); CHECK(hipEventSynchronize(b));
-        float ms; CHECK(hipEventElapsedTime(&ms, a, b)); best = ms < best ? ms : best;
+__global__ void fill_i8(int8_t* p, size_t n, uint64_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t h = splitmix64(seed + i);
+        p[i] = (int8_t)((int)(h % 255) - 127);
     }
-    return best;
+}
+__global__ void fill_f32(float* p, size_t n, float v) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 1000000, nq = argc > 2 ? atoi(argv[2]) : 1000, ld = 768;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 6;
     const uint32_t qpad = (nq + 255) / 256 * 256, npad = (n + 255) / 256 * 256;
-    uint16_t *A, *B; float* tau; uint64_t* cand; uint32_t* cnt;
+    uint8_t *A16, *B16, *A8, *B8; float *tau, *as, *bs; uint64_t* cand; uint32_t* cnt;
     const uint32_t cap = 1024;
-    CHECK(hipMalloc(&A, (size_t)npad * ld * 2)); CHECK(hipMalloc(&B, (size_t)qpad * ld * 2));
+    CHECK(hipMalloc(&A16, (size_t)npad * ld * 2)); CHECK(hipMalloc(&B16, (size_t)qpad * ld * 2));
+    CHECK(hipMalloc(&A8, (size_t)npad * ld)); CHECK(hipMalloc(&B8, (size_t)qpad * ld));
+    CHECK(hipMalloc(&as, npad / 32 * 4)); CHECK(hipMalloc(&bs, qpad * 4));
     CHECK(hipMalloc(&tau, qpad * 4)); CHECK(hipMalloc(&cand, (size_t)qpad * cap * 8)); CHECK(hipMalloc(&cnt, qpad * 4));
-    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, A, (size_t)npad * ld, 1);
-    hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, B, (size_t)qpad * ld, 2);
-    const float tauv = argc > 3 ? atof(argv[3]) : 1e9f;
-    std::vector<float> ht(qpad, tauv);
-    CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, (uint16_t*)A16, (size_t)npad * ld, 1);
+    hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, (uint16_t*)B16, (size_t)qpad * ld, 2);
+    hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
+    hipLaunchKernelGGL(fill_i8, dim3(1024), dim3(256), 0, 0, (int8_t*)B8, (size_t)qpad * ld, 4);
+    hipLaunchKernelGGL(fill_f32, dim3(256), dim3(256), 0, 0, as, (size_t)npad / 32, 1.0f / (127.0f * 16.0f));
+    hipLaunchKernelGGL(fill_f32, dim3(16), dim3(256), 0, 0, bs, (size_t)qpad, 1.0f / (127.0f * 16.0f));
+    CHECK(hipDeviceSynchronize());
     GemmArgs g{};
-    g.A = A; g.a_row_stride = ld; g.n_rows = n; g.B = B; g.ld = ld; g.n_qt = qpad / 256;
-    g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
+    g.n_rows = n; g.a_row_mult = 1; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
+    g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double flops = 2.0 * nq * (double)n * ld;
-    struct V { const char* name; void (*k)(GemmArgs); float tau; std::vector<float> t; };
+    struct V { const char* name; void (*k)(GemmArgs); bool i8; float tau; std::vector<float> t; };
     std::vector<V> vs = {
-        {"v2 tau=inf", k_gemm_filter2<true, 0>, 1e9f, {}},
-        {"v4 tau=inf", k_gemm_filter4<true, 0>, 1e9f, {}},
-        {"v2 tau=0.05", k_gemm_filter2<true, 0>, 0.05f, {}},
-        {"v4 tau=0.05", k_gemm_filter4<true, 0>, 0.05f, {}},
-        {"v4 tau=0.0415", k_gemm_filter4<true, 0>, 0.0415f, {}},
-        {"v4 no-DMA", k_gemm_filter4<true, 1>, 1e9f, {}},
-        {"v4 DMA-only", k_gemm_filter4<true, 3>, 1e9f, {}},
+        {"bf16 tau=inf", k_filter<OpBF16, true, 0>, false, 1e9f, {}},
+        {"bf16 tau=0.0415", k_filter<OpBF16, true, 0>, false, 0.0415f, {}},
+        {"bf16 no-DMA", k_filter<OpBF16, true, 1>, false, 1e9f, {}},
+        {"bf16 DMA-only", k_filter<OpBF16, true, 3>, false, 1e9f, {}},
+        {"i8 tau=inf", k_filter<OpI8, true, 0>, true, 1e9f, {}},
+        {"i8 tau=0.125", k_filter<OpI8, true, 0>, true, 0.125f, {}},
+        {"i8 no-DMA", k_filter<OpI8, true, 1>, true, 1e9f, {}},
+        {"i8 DMA-only", k_filter<OpI8, true, 3>, true, 1e9f, {}},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
-    const int rounds = argc > 3 ? atoi(argv[3]) : 5;
     for (int r = 0; r < rounds; ++r) {
         for (auto& v : vs) {
+            g.A = v.i8 ? A8 : A16; g.B = v.i8 ? B8 : B16;
+            g.row_bytes = v.i8 ? ld : 2 * ld; g.a_stride = g.row_bytes;
             std::vector<float> ht(qpad, v.tau);
             CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
             CHECK(hipMemset(cnt, 0, qpad * 4));
@@ -82,7 +87,8 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
         std::sort(v.t.begin(), v.t.end());
         float med = v.t[v.t.size() / 2], mn = v.t[0];
-        printf("%-18s median %7.3f ms  min %7.3f ms  (%6.1f TF/s at median)\n", v.name, med, mn, flops / (med * 1e-3) / 1e12);
+        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f T(FL)OP/s at median)\n", v.name, med, mn,
+               flops / (med * 1e-3) / 1e12);
     }
     return 0;
 }

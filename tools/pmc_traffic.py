@@ -4,7 +4,7 @@ HBM bytes per launch of the dominant kernel = FETCH_SIZE * 1024 * 2 + WRITE_SIZE
 on gfx950 FETCH_SIZE (KB) reports half of the bytes of a wide coalesced read
 (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for 16-B stores.  FETCH_SIZE and
 WRITE_SIZE are collected in separate passes (TCC counter slots).
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <rows> <queries> <out.json>
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <rows> <queries> <filter> <out.json>
 """
 import csv
 import glob
@@ -24,11 +24,11 @@ def per_kernel(d, counter):
 
 
 def main():
-    fdir, wdir, rows, queries, out = sys.argv[1:6]
+    fdir, wdir, rows, queries, filt, out = sys.argv[1:7]
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
-    emit = [k for k in fetch if "gemm_filter" in k and "<true" in k]
-    res = {"rows": int(rows), "queries": int(queries), "kernels": {}}
+    emit = [k for k in fetch if "k_filter" in k and "true" in k]
+    res = {"rows": int(rows), "queries": int(queries), "filter": filt, "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k)
         w = write.get(k)
