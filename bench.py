@@ -184,7 +184,8 @@ def main():
                 "qps_over_full_corpus": round(Q / (ms_per_step * 1e-3), 2),
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
-            "p50_config": f"1 query over {n_total} rows (exact scan, HBM-bound)",
+            "p50_config": f"1 query over {n_total} rows" + (
+                " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else " (exact f32 scan, HBM-bound)"),
             "roofline": {
                 "bound": "mfma", "kernel": kname,
                 "achieved": round(achieved, 2) if achieved else None,
@@ -203,19 +204,31 @@ def main():
                 "scan_fallback": round(prof.scan_ms / args.steps, 4),
                 "local_search_total": round(prof.search_ms / args.steps, 4),
             },
-            "p50_scan_kernel_ms": round(prof_scan.scan_ms / max(prof_scan.scan_launches, 1), 4),
+            "p50_kernels_ms": {
+                "filter_emit": round(prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1), 4),
+                "filter_sample": round(prof_scan.gemm_sample_ms / max(prof_scan.gemm_sample_launches, 1), 4),
+                "exact_scan": round(prof_scan.scan_ms / max(prof_scan.scan_launches, 1), 4),
+                "local_search_total": round(prof_scan.search_ms / max(prof_scan.searches, 1), 4)},
             "fallback_queries_per_step": stats_fb / args.steps,
             "candidates_per_query": st.n_candidates,
             "self_query_rank1": self_ok,
             "emitted_per_query": round(st.n_emitted / max(Q, 1), 1),
             "row_ebound": round(float(st.row_ebound), 6),
         }
-        # HBM roofline of the single-query scan kernel (bytes = N*d*4 per query).
-        scan_ms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)
-        if scan_ms > 0:
-            gbs = n_local * D * 4 / (scan_ms * 1e-3) / 1e9
-            out["roofline_scan"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM / 1e9,
-                                    "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4)}
+        # HBM roofline of the single-query (p50) kernel: the int8 skinny filter reads the
+        # int8 rows (N*ld bytes per query batch); the bf16 index uses the exact f32 scan
+        # (N*ld*4 bytes).
+        if args.filter == "i8":
+            kms = prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1)
+            kbytes, kn = n_local * ((D + 63) // 64 * 64), "k_filter_skinny<true>"
+        else:
+            kms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)
+            kbytes, kn = n_local * ((D + 63) // 64 * 64) * 4, "k_scan_exact<1,1>"
+        if kms > 0:
+            gbs = kbytes / (kms * 1e-3) / 1e9
+            out["roofline_p50"] = {"bound": "hbm", "kernel": kn, "achieved": round(gbs, 1),
+                                   "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4),
+                                   "bytes_per_launch": kbytes, "avg_launch_ms": round(kms, 4)}
 
     # Parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on the same corpus.
     if rank == 0 and world == 1 and (args.verify or not args.no_cpu_baseline):

@@ -73,6 +73,41 @@ __device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+    int lo = __shfl((int)(uint32_t)x, src, kWave);
+    int hi = __shfl((int)(uint32_t)(x >> 32), src, kWave);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int m) {
+    int lo = __shfl_xor((int)(uint32_t)x, m, kWave);
+    int hi = __shfl_xor((int)(uint32_t)(x >> 32), m, kWave);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// Ascending bitonic sort of one key per lane across the wave (21 compare-exchange steps).
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t y = shfl_xor64(x, j);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+        }
+    }
+    return x;
+}
+// A bitonic sequence of 64 keys (one per lane) -> ascending.
+__device__ __forceinline__ uint64_t bitonic_clean64(uint64_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+        const uint64_t y = shfl_xor64(x, j);
+        x = (lane & j) ? (x < y ? y : x) : (x < y ? x : y);
+    }
+    return x;
+}
+
 template <int E>
 struct WaveTopK {
     uint64_t v[E];
@@ -109,10 +144,33 @@ struct WaveTopK {
             v[e] = (p > pos) ? prev : ((p == pos) ? x : v[e]);
         }
     }
-    // Offer one key per lane (kKeyNone = nothing); keeps the smallest `k` keys seen.
-    // `thr` is the current k-th smallest key, updated.
+    // Merge a batch of up to 64 keys (one per lane, kKeyNone = nothing) into the list:
+    // bitonic sort of the batch across the wave, then a merge cascade down the E registers
+    // (min/max against the reversed batch leaves two bitonic halves, each sorted by a
+    // 6-step half-cleaner; the larger half moves on to the next register).
+    __device__ __forceinline__ void merge_batch(uint64_t x) {
+        const int lane = lane_id();
+        x = wave_sort64(x);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint64_t xr = shfl64(x, 63 - lane);
+            const uint64_t lo = v[e] < xr ? v[e] : xr;
+            const uint64_t hi = v[e] < xr ? xr : v[e];
+            v[e] = bitonic_clean64(lo);
+            if (e + 1 < E) x = bitonic_clean64(hi);
+        }
+    }
+    // Offer one key per lane (kKeyNone = nothing); keeps the smallest `k` keys seen
+    // (k <= 64*E).  `thr` is the current k-th smallest key, updated.  A few passing keys
+    // are inserted one by one; a larger batch is merged.
     __device__ __forceinline__ void offer(uint64_t x, int k, uint64_t& thr) {
         uint64_t m = __ballot(x < thr);
+        if (!m) return;
+        if (__popcll(m) > 3) {
+            merge_batch(x < thr ? x : kKeyNone);
+            thr = at(k - 1);
+            return;
+        }
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;

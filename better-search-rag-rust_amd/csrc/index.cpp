@@ -264,7 +264,28 @@ int bsr_index_get_many_impl(const bsr_index* ix, uint64_t offset, uint64_t count
 // ---------------------------------------------------------------------------------------
 // search
 // ---------------------------------------------------------------------------------------
-static int run_exact_scan(bsr_index* ix, const std::vector<int32_t>& ids, uint32_t k) {
+// Exact full scan of n_ids queries whose ids are the device list `ids` (groups of kScanQF;
+// an id list padded to a multiple of kScanQF with valid ids).
+static int run_exact_scan(bsr_index* ix, const int32_t* ids, uint32_t n_ids, uint32_t k) {
+    if (!n_ids) return BSR_OK;
+    const uint32_t groups = (n_ids + kScanQF - 1) / kScanQF;
+    const uint32_t grid = scan_grid_for(ix->n);
+    BSR_TRY(ix->part.ensure((size_t)grid * kScanQF * k * sizeof(uint64_t)));
+    ev_begin(ix, ix->ev_scan);
+    for (uint32_t g = 0; g < groups; ++g) {
+        const uint32_t nqf = std::min(kScanQF, n_ids - g * kScanQF);
+        const int32_t* qid = ids + (size_t)g * kScanQF;
+        BSR_HIP(launch_scan_exact(ix->rows.as<float>(), ix->ld, ix->dim, ix->n, ix->na.as<float>(),
+                                  ix->qf32.as<float>(), qid, nqf, ix->nb.as<float>(), k, grid,
+                                  ix->part.as<uint64_t>(), ix->stream));
+        BSR_HIP(launch_merge_parts(ix->part.as<uint64_t>(), grid, qid, nqf, k, ix->keys.as<uint64_t>(), ix->stream));
+    }
+    ev_end(ix, ix->ev_scan);
+    return BSR_OK;
+}
+
+// The same for a host list of query ids (the fallback queries of a batch).
+static int run_exact_scan_list(bsr_index* ix, const std::vector<int32_t>& ids, uint32_t k) {
     if (ids.empty()) return BSR_OK;
     const uint32_t groups = (uint32_t)((ids.size() + kScanQF - 1) / kScanQF);
     std::vector<int32_t> padded((size_t)groups * kScanQF);
@@ -276,23 +297,13 @@ static int run_exact_scan(bsr_index* ix, const std::vector<int32_t>& ids, uint32
     BSR_TRY(ix->qids.ensure(padded.size() * sizeof(int32_t)));
     BSR_HIP(hipMemcpyAsync(ix->qids.p, padded.data(), padded.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                            ix->stream));
-    const uint32_t grid = scan_grid_for(ix->n);
-    BSR_TRY(ix->part.ensure((size_t)grid * kScanQF * k * sizeof(uint64_t)));
-    ev_begin(ix, ix->ev_scan);
-    for (uint32_t g = 0; g < groups; ++g) {
-        const uint32_t nqf = (uint32_t)std::min<size_t>(kScanQF, ids.size() - (size_t)g * kScanQF);
-        const int32_t* qid = ix->qids.as<int32_t>() + (size_t)g * kScanQF;
-        BSR_HIP(launch_scan_exact(ix->rows.as<float>(), ix->ld, ix->dim, ix->n, ix->na.as<float>(),
-                                  ix->qf32.as<float>(), qid, nqf, ix->nb.as<float>(), k, grid,
-                                  ix->part.as<uint64_t>(), ix->stream));
-        BSR_HIP(launch_merge_parts(ix->part.as<uint64_t>(), grid, qid, nqf, k, ix->keys.as<uint64_t>(), ix->stream));
-    }
-    ev_end(ix, ix->ev_scan);
-    return BSR_OK;
+    return run_exact_scan(ix, ix->qids.as<int32_t>(), (uint32_t)ids.size(), k);
 }
 
-// Candidate stage (steps 2-5) for every query of the batch.
+// Candidate stage (steps 2-5) for every query of the batch.  Batches of at most 16
+// queries on an int8 index use the skinny (HBM-bound, no LDS) filter kernels.
 static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
+    const bool skinny = ix->op == kFilterI8 && nq <= kSkinnyMaxQ;
     const uint32_t kp = 64u * ((k + 54u + 63u) / 64u) - 1u;  // k' candidates, (k'+1) % 64 == 0
     const uint32_t cap = 16u * (kp + 1u);
     const uint32_t ks = (kp + 1u) / 8u;
@@ -334,7 +345,8 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         g.s_ld = s_ld;
         g.s_compact = compact ? 1u : 0u;
         ev_begin(ix, ix->ev_sample);
-        BSR_HIP(launch_filter_sample(ix->op, g, ix->stream));
+        if (skinny) BSR_HIP(launch_filter_skinny_sample(g, ix->stream));
+        else BSR_HIP(launch_filter_sample(ix->op, g, ix->stream));
         ev_end(ix, ix->ev_sample);
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
                                   ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
@@ -352,7 +364,8 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cnt = ix->cnt.as<uint32_t>();
     g.cap = cap;
     ev_begin(ix, ix->ev_emit);
-    BSR_HIP(launch_filter_emit(ix->op, g, ix->stream));
+    if (skinny) BSR_HIP(launch_filter_skinny_emit(g, ix->stream));
+    else BSR_HIP(launch_filter_emit(ix->op, g, ix->stream));
     ev_end(ix, ix->ev_emit);
     ev_begin(ix, ix->ev_select);
     BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(), kp,
@@ -391,6 +404,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     BSR_TRY(ebound.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(qflags.ensure((size_t)qpad * sizeof(uint32_t)));
     BSR_TRY(status.ensure(kStWords * sizeof(uint32_t)));
+    BSR_TRY(qids_id.ensure((size_t)qpad * sizeof(int32_t)));
     BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
 
     ev_begin(ix, ev_total);
@@ -400,7 +414,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
         qsrc = q_in.as<float>();
     }
-    BSR_HIP(hipMemsetAsync(status.p, 0, kStWords * sizeof(uint32_t), stream));
+    // status words are zeroed by the previous search's finalize kernel (or here once)
+    if (!status_clean) BSR_HIP(hipMemsetAsync(status.p, 0, kStWords * sizeof(uint32_t), stream));
+    status_clean = false;
+    // int8 indexes filter every batch (small ones with the skinny kernels); bf16 indexes
+    // only batches of >= 16 queries (smaller ones take the exact scan).
+    const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter &&
+                            (op == kFilterI8 || nq >= kMinBatchForFilter);
     QueryPrepArgs qa{};
     qa.q = qsrc;
     qa.nq = nq;
@@ -415,18 +435,18 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     qa.qscale = qscale.as<float>();
     qa.ebound = ebound.as<float>();
     qa.qflags = qflags.as<uint32_t>();
+    qa.qids = qids_id.as<int32_t>();
     qa.status = status.as<uint32_t>();
+    qa.with_op = use_filter;
     BSR_HIP(launch_query_prep(qa, stream));
 
-    const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter && nq >= kMinBatchForFilter;
     std::vector<int32_t> exact_ids;
     if (n == 0) {
         // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
         BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
     } else if (!use_filter) {
-        for (uint32_t q = 0; q < nq; ++q) exact_ids.push_back((int32_t)q);
         stats.n_exact_direct = nq;
-        BSR_TRY(run_exact_scan(ix, exact_ids, k));
+        BSR_TRY(run_exact_scan(ix, qids_id.as<int32_t>(), nq, k));
     } else {
         BSR_TRY(run_filter(ix, nq, qpad, k));
     }
@@ -460,11 +480,12 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
                 if (h_qflags[q] & kQueryNoApprox) ++stats.n_exact_direct;
                 else ++stats.n_fallback;
             }
-            BSR_TRY(run_exact_scan(ix, exact_ids, k));
+            BSR_TRY(run_exact_scan_list(ix, exact_ids, k));
         }
     }
     BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, o_idx.as<uint64_t>(), o_dist.as<float>(),
-                            o_cnt.as<uint32_t>(), stream));
+                            o_cnt.as<uint32_t>(), status.as<uint32_t>(), stream));
+    status_clean = true;
     ev_end(ix, ev_total);
     return BSR_OK;
 }

@@ -75,7 +75,8 @@ struct bsr_index {
 
     // per-search scratch
     bsr::DevBuf q_in, qf32, nb, qop, qscale, ebound, qflags, status, tau, S, cand, cnt, cand_rows,
-        ncand, tau_excl, keys, fail, part, qids, o_idx, o_dist, o_cnt, tmp;
+        ncand, tau_excl, keys, fail, part, qids, qids_id, o_idx, o_dist, o_cnt, tmp;
+    bool status_clean = false;  // status words known to be zero (finalize of the last search)
     std::vector<uint32_t> h_qflags, h_fail;
 
     bsr_search_stats stats{};

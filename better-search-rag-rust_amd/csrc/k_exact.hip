@@ -259,34 +259,55 @@ __global__ __launch_bounds__(256, 2) void k_scan_exact(const float* __restrict__
     }
 }
 
-// Per scanned query: merge the per-block lists of k_scan_exact into out_keys[qid].
+// Per scanned query: merge the per-block lists of k_scan_exact into out_keys[qid].  Four
+// waves each take a quarter of the grid's lists (loads issued 4 deep), then wave 0 merges
+// the four wave lists through LDS.
 template <int E>
-__global__ __launch_bounds__(64) void k_merge_parts(const uint64_t* __restrict__ part, uint32_t grid,
-                                                    const int32_t* __restrict__ qids, uint32_t qf,
-                                                    uint32_t nqf, uint32_t k,
-                                                    uint64_t* __restrict__ out_keys) {
+__global__ __launch_bounds__(256) void k_merge_parts(const uint64_t* __restrict__ part, uint32_t grid,
+                                                     const int32_t* __restrict__ qids, uint32_t qf,
+                                                     uint32_t nqf, uint32_t k,
+                                                     uint64_t* __restrict__ out_keys) {
+    __shared__ uint64_t lk[4][64 * E];
     const uint32_t j = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (j >= nqf) return;
     WaveTopK<E> L;
     L.init();
     uint64_t thr = kKeyNone;
     const uint64_t total = (uint64_t)grid * k;
-    for (uint64_t base = 0; base < total; base += kWave) {
-        const uint64_t i = base + threadIdx.x;
-        uint64_t key = kKeyNone;
-        if (i < total) {
-            const uint64_t g = i / k, e = i - g * k;
-            key = part[(g * qf + j) * k + e];
-        }
-        L.offer(key, (int)k, thr);
+    const uint64_t per = (total + 3) / 4, lo = w * per, hi = lo + per < total ? lo + per : total;
+    auto key_at = [&](uint64_t i) -> uint64_t {
+        if (i >= hi) return kKeyNone;
+        const uint64_t g = i / k, e = i - g * k;
+        return part[(g * qf + j) * k + e];
+    };
+    for (uint64_t base = lo; base < hi; base += 4 * kWave) {
+        uint64_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = key_at(base + u * kWave + lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) L.offer(x[u], (int)k, thr);
     }
-    L.store(out_keys + (uint64_t)qids[j] * k, (int)k);
+    L.store(&lk[w][0], (int)k);
+    __syncthreads();
+    if (w == 0) {
+        WaveTopK<E> M;
+        M.init();
+        uint64_t mt = kKeyNone;
+        for (int src = 0; src < 4; ++src)
+            for (uint32_t b = 0; b < k; b += kWave) {
+                const uint32_t i = b + lane;
+                M.offer(i < k ? lk[src][i] : kKeyNone, (int)k, mt);
+            }
+        M.store(out_keys + (uint64_t)qids[j] * k, (int)k);
+    }
 }
 
 __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* __restrict__ out_idx, float* __restrict__ out_dist,
-                           uint32_t* __restrict__ out_count) {
+                           uint32_t* __restrict__ out_count, uint32_t* __restrict__ status) {
     const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (e < kStWords) status[e] = 0;  // read back by the host before this kernel runs
     if (e >= (uint64_t)nq * k) return;
     const uint32_t q = (uint32_t)(e / k), i = (uint32_t)(e - (uint64_t)q * k);
     const uint32_t cnt = (uint64_t)k < n ? k : (uint32_t)n;
@@ -379,7 +400,7 @@ hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t
     const uint32_t qf = nqf <= 1 ? 1 : nqf <= 2 ? 2 : nqf <= 4 ? 4 : 8;
     const uint32_t e = (k + 63) / 64;
 #define BSR_MERGE(E)                                                                              \
-    hipLaunchKernelGGL(k_merge_parts<E>, dim3(nqf), dim3(64), 0, s, part, grid, qids, qf, nqf, k, \
+    hipLaunchKernelGGL(k_merge_parts<E>, dim3(nqf), dim3(256), 0, s, part, grid, qids, qf, nqf, k, \
                        out_keys)
     switch (e) {
         case 1: BSR_MERGE(1); break;
@@ -392,10 +413,11 @@ hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t
 }
 
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n, uint64_t offset,
-                           uint64_t* out_idx, float* out_dist, uint32_t* out_count, hipStream_t s) {
+                           uint64_t* out_idx, float* out_dist, uint32_t* out_count, uint32_t* status,
+                           hipStream_t s) {
     const uint64_t total = (uint64_t)nq * k;
     hipLaunchKernelGGL(k_finalize, dim3(grid_for(total, 256)), dim3(256), 0, s, keys, nq, k, n, offset,
-                       out_idx, out_dist, out_count);
+                       out_idx, out_dist, out_count, status);
     return hipGetLastError();
 }
 

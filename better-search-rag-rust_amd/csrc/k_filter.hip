@@ -228,10 +228,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
     uint32_t ti = 0, kt = 0;
     for (uint32_t jj = 0; jj < J; ++jj) {
         const bool iss = VAR != 1 && jj + 3 < J;
-        // ---- first half: kk = 0 MFMAs, kk = 1 reads, A-half DMA of slice jj+3
-        read_frags(jj, 1, fa1, fb1);
-        __builtin_amdgcn_sched_barrier(0);
+        // ---- first half: kk = 0 MFMAs, kk = 1 reads, A-half DMA of slice jj+3.  The
+        // reads go after the first MFMA group: hipcc puts a conservative lgkmcnt(0) in
+        // front of an MFMA whose operands came from ds_read (it cannot see the barrier's
+        // inline wait), which must not cover reads issued just before it.
         mfma4(fa0, fb0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(jj, 1, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
         if (iss) dma_a(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -257,10 +260,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         } else {
             mid_barrier<0>();
         }
-        const bool next = jj + 1 < J;
-        if (next) read_frags(jj + 1, 0, fa0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
+        // ---- second half: kk = 1 MFMAs, next slice's kk = 0 reads, B-half DMA
         mfma4(fa1, fb1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (jj + 1 < J) read_frags(jj + 1, 0, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
         if (iss) dma_b(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -316,6 +319,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 #pragma unroll
                         for (int r = 1; r < 16; ++r) mxv = mxv > acc[m][n][r] ? mxv : acc[m][n][r];
                         if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
+                            // per-lane pass mask, then only the passing (lane, register)
+                            // pairs append
                             uint32_t mask = 0;
 #pragma unroll
                             for (int r = 0; r < 16; ++r)
@@ -364,6 +369,103 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
             const uint32_t q = qt * BN + eq[i];
             const uint32_t gp = atomicAdd(p.cnt + q, 1u);
             if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Skinny int8 filter for batches of at most 16 queries (single-query latency path): the
+// work is HBM-bound (1 byte per element), so there is no LDS staging.  Each wave walks
+// groups of 32 tile rows; per 64-byte K step a lane loads its 16-byte A fragments straight
+// from HBM (16 rows x 64 B per v_mfma_i32_16x16x64_i8 operand; lane l: row l&15, bytes
+// 16(l>>4)..+15) and the matching query fragment (L1-resident), 8 K steps of loads in
+// flight before their MFMAs.  The 16x16 accumulator has query l&15 on the lane and rows
+// 4(l>>4)+i in its registers.  Epilogue as k_filter: SAMPLE stores every score or the
+// maximum over the 32 rows of the group; EMIT appends (score, row) keys of rows reaching
+// tau straight to the per-query global lists (emission is rare).
+// ------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) int i32x4_acc_t;
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
+    constexpr int KC = 8;  // K steps of loads in flight
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t q = lane & 15, h = lane >> 4;
+    const uint32_t nk = p.row_bytes / kSliceB;
+    const uint32_t n_groups = (p.n_rows + 31) / 32;
+    const uint32_t nwaves = gridDim.x * 4;
+    const float sbq = p.b_scale[q];
+    const float tauq = EMIT ? p.tau[q] : 0.0f;
+    const uint8_t* bq = p.B + (uint64_t)q * p.row_bytes + h * 16;
+    for (uint32_t g = blockIdx.x * 4 + w; g < n_groups; g += nwaves) {
+        uint32_t r0 = g * 32 + q, r1 = g * 32 + 16 + q;
+        r0 = r0 < p.n_rows ? r0 : p.n_rows - 1;  // tail rows: clamped, never emitted
+        r1 = r1 < p.n_rows ? r1 : p.n_rows - 1;
+        const uint8_t* a0 = p.A + (uint64_t)r0 * p.a_stride + h * 16;
+        const uint8_t* a1 = p.A + (uint64_t)r1 * p.a_stride + h * 16;
+        i32x4_acc_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+        for (uint32_t s0 = 0; s0 < nk; s0 += KC) {
+            i32x4_t fa0[KC], fa1[KC], fb[KC];
+#pragma unroll
+            for (int s = 0; s < KC; ++s) {
+                if (s0 + s < nk) {
+                    fa0[s] = *reinterpret_cast<const i32x4_t*>(a0 + (s0 + s) * kSliceB);
+                    fa1[s] = *reinterpret_cast<const i32x4_t*>(a1 + (s0 + s) * kSliceB);
+                    fb[s] = *reinterpret_cast<const i32x4_t*>(bq + (s0 + s) * kSliceB);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < KC; ++s) {
+                if (s0 + s < nk) {
+                    acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa0[s], fb[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa1[s], fb[s], acc1, 0, 0, 0);
+                }
+            }
+        }
+        // rows of register i: tile 0 -> g*32 + 4h + i, tile 1 -> g*32 + 16 + 4h + i
+        if constexpr (EMIT) {
+            const float sc = p.a_scale[g];  // emit: tile row == corpus row, one 32-row block
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v[i] = ((float)acc0[i] * sc) * sbq;
+                v[4 + i] = ((float)acc1[i] * sc) * sbq;
+            }
+            float mx = v[0];
+#pragma unroll
+            for (int i = 1; i < 8; ++i) mx = fmaxf(mx, v[i]);
+            if (__ballot(mx >= tauq)) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t row = g * 32 + (i >> 2) * 16 + 4 * h + (i & 3);
+                    if (v[i] >= tauq && row < p.n_rows) {
+                        const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                        if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v[i], row);
+                    }
+                }
+            }
+        } else {
+            // sample: tile row r is corpus row r * a_row_mult, scale block r * mult / 32
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t tr = g * 32 + (i >> 2) * 16 + 4 * h + (i & 3);
+                tr = tr < p.n_rows ? tr : p.n_rows - 1;
+                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                v[i] = ((float)(i < 4 ? acc0[i] : acc1[i - 4]) * sc) * sbq;
+            }
+            float* srow = p.S + (uint64_t)q * p.s_ld;
+            if (!p.s_compact) {
+                *reinterpret_cast<float4*>(srow + g * 32 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(srow + g * 32 + 16 + 4 * h) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                float mx = v[0];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) mx = fmaxf(mx, v[i]);
+                mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+                mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                if (h == 0) srow[g] = mx;
+            }
         }
     }
 }
@@ -437,9 +539,15 @@ __global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__
     L.init();
     uint64_t thr = kKeyNone;
     const uint64_t* src = cand + (uint64_t)q * cap;
-    for (uint32_t base = 0; base < c; base += kWave) {
-        const uint32_t i = base + threadIdx.x;
-        L.offer(i < c ? src[i] : kKeyNone, (int)kp + 1, thr);
+    for (uint32_t base = 0; base < c; base += 4 * kWave) {
+        uint64_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = base + u * kWave + threadIdx.x;
+            x[u] = i < c ? src[i] : kKeyNone;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) L.offer(x[u], (int)kp + 1, thr);
     }
     const uint32_t nc = c < kp ? c : kp;
 #pragma unroll
@@ -460,6 +568,19 @@ __global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__
 static uint32_t filter_grid(uint32_t n_qt) {
     const uint32_t per_xcd = n_qt >= 32 ? n_qt : (32 / n_qt) * n_qt;
     return 8 * per_xcd;
+}
+
+static uint32_t skinny_grid(uint32_t n_rows) {
+    const uint32_t groups = (n_rows + 31) / 32, wgs = (groups + 3) / 4;
+    return wgs < 768 ? (wgs ? wgs : 1) : 768;  // 3 workgroups per CU (VGPR-limited occupancy)
+}
+hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_filter_skinny<false>, dim3(skinny_grid(a.n_rows)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_filter_skinny<true>, dim3(skinny_grid(a.n_rows)), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s) {

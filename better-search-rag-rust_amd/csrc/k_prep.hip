@@ -219,90 +219,81 @@ __global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ ro
 }
 
 // ------------------------------------------------------------------------------------
-// Queries.
-// k_query_norms: 64 queries per wave, 64-column chunks staged through LDS (coalesced reads),
-// each lane then walks its own query in index order: |b| exactly as src/metrics.rs:155,
-// finiteness and eligibility for the filter.
+// Queries: one wave per (padded) query, the whole preparation in one kernel.
+//   1. the caller's row -> LDS (coalesced) and the padded f32 copy qf32[q] (zeros past dim)
+//   2. lane 0 walks the row in index order: |b| exactly as src/metrics.rs:155 (sequential
+//      f32 sum of squares from -0.0, correctly rounded sqrt), finiteness
+//   3. flags, the identity query-id list of the exact scan (min(q, nq-1))
+//   4. the filter operand from the LDS copy:
+//        bf16: bf16_rne(b_i / |b|), E_q = the constant bf16 bound
+//        int8: x = b/|b| (double), s = smallest f32 >= max|x_i|/127, q_i = rint(x_i/s),
+//              eb = ||x - s q||_2, E_q = ea + eb + ea*eb + 1.5e-4 (ea: the row side; 1.5e-4
+//              covers the reference's own f32 rounding, <= 9.3e-5, and the two f32 roundings
+//              of the filter's score)
+//      queries the filter cannot serve (pad, zero/tiny/huge |b|) get a zero operand and
+//      E_q = inf.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_query_norms(const float* __restrict__ q, uint32_t nq, uint32_t qpad,
-                                                    uint32_t dim, FilterOp op, float* __restrict__ nb,
-                                                    float* __restrict__ ebound,
-                                                    uint32_t* __restrict__ qflags,
-                                                    uint32_t* __restrict__ status) {
-    __shared__ float tile[64][65];
-    const int lane = threadIdx.x;
-    const uint32_t q0 = blockIdx.x * 64, qi = q0 + lane;
-    float acc = -0.0f;
-    bool bad = false;
-    for (uint32_t c0 = 0; c0 < dim; c0 += 64) {
-        const uint32_t c = c0 + lane;
-        for (int r = 0; r < 64; ++r) {
-            const uint32_t qq = q0 + r;
-            tile[r][lane] = (qq < nq && c < dim) ? q[(uint64_t)qq * dim + c] : 0.0f;
-        }
-        __syncthreads();
-        const uint32_t nv = dim - c0 < 64 ? dim - c0 : 64;
-        for (uint32_t i = 0; i < nv; ++i) {
-            const float x = tile[lane][i];
-            bad = bad || !isfinite(x);
-            acc = acc + x * x;
-        }
-        __syncthreads();
-    }
-    if (qi >= qpad) return;
-    if (qi >= nq) {
-        nb[qi] = 0.0f;
-        qflags[qi] = kQueryNoApprox;
-        ebound[qi] = INFINITY;
-        return;
-    }
-    const float m = __builtin_sqrtf(acc);
-    nb[qi] = m;
-    const bool approx_ok = !bad && isfinite(m) && m >= 1e-18f && m <= 1e18f;
-    const uint32_t f = (bad ? kQueryNonFinite : 0u) | (approx_ok ? 0u : kQueryNoApprox);
-    qflags[qi] = f;
-    // bf16: the constant bound; i8: written by k_query_i8
-    if (op == kFilterBF16) ebound[qi] = approx_ok ? (float)kEBoundBF16 : INFINITY;
-    if (f & kQueryNonFinite) atomicOr(status + kStQueryFlags, kQueryNonFinite);
-}
+constexpr uint32_t kQueryLdsFloats = 8192;  // rows up to 8192 floats are staged in LDS
 
-// Padded f32 copy [qpad][ld] and, for the bf16 filter, the normalised bf16 copy.
-__global__ void k_query_convert(const float* __restrict__ q, uint32_t nq, uint32_t qpad, uint32_t dim,
-                                uint32_t ld, const float* __restrict__ nb,
-                                const uint32_t* __restrict__ qflags, float* __restrict__ qf32,
-                                uint16_t* __restrict__ qbf) {
-    const uint64_t total = (uint64_t)qpad * ld;
-    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
-         e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t qi = (uint32_t)(e / ld), c = (uint32_t)(e - (uint64_t)qi * ld);
-        const float v = (qi < nq && c < dim) ? q[(uint64_t)qi * dim + c] : 0.0f;
-        qf32[e] = v;
-        if (qbf) {
-            const bool ok = qi < nq && c < dim && !(qflags[qi] & kQueryNoApprox);
-            qbf[e] = ok ? f32_to_bf16_rne(v / nb[qi]) : (uint16_t)0;
-        }
-    }
-}
-
-// int8 query operand, one wave per query (same construction as k_rows_to_i8 with a
-// per-query scale), and the per-query certification bound
-//   E_q = ea + eb + ea*eb + 1.5e-4
-// (ea: row side, eb: this query; 1.5e-4 covers the reference's own f32 rounding, <= 9.3e-5,
-// and the two f32 roundings of the filter's score).
-__global__ __launch_bounds__(64) void k_query_i8(const float* __restrict__ qf32, uint32_t nq, uint32_t dim,
-                                                 uint32_t ld, const uint32_t* __restrict__ qflags,
-                                                 const uint32_t* __restrict__ ea_max,
-                                                 int8_t* __restrict__ qi8, float* __restrict__ qscale,
-                                                 float* __restrict__ ebound) {
+__global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, uint32_t nq, uint32_t dim,
+                                                   uint32_t ld, FilterOp op, bool with_op,
+                                                   const uint32_t* __restrict__ ea_max,
+                                                   float* __restrict__ qf32, float* __restrict__ nb,
+                                                   void* __restrict__ qop, float* __restrict__ qscale,
+                                                   float* __restrict__ ebound, uint32_t* __restrict__ qflags,
+                                                   int32_t* __restrict__ qids, uint32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) float row[kQueryLdsFloats];
+    __shared__ float s_mag;
+    __shared__ uint32_t s_flags;
     const uint32_t qi = blockIdx.x;
     const int lane = threadIdx.x;
-    const float* b = qf32 + (uint64_t)qi * ld;
-    int8_t* o = qi8 + (uint64_t)qi * ld;
-    const bool ok = qi < nq && !(qflags[qi] & kQueryNoApprox);
+    const bool real = qi < nq;
+    const bool staged = ld <= kQueryLdsFloats;
+    const float* src = q + (uint64_t)qi * dim;
+    float* dst = qf32 + (uint64_t)qi * ld;
+    for (uint32_t c = lane; c < ld; c += kWave) {
+        const float v = (real && c < dim) ? src[c] : 0.0f;
+        dst[c] = v;
+        if (staged) row[c] = v;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        float acc = -0.0f;
+        bool bad = false;
+        if (real) {
+            for (uint32_t i = 0; i < dim; ++i) {
+                const float x = staged ? row[i] : src[i];
+                bad = bad || !isfinite(x);
+                acc = acc + x * x;
+            }
+        }
+        const float m = __builtin_sqrtf(acc);
+        const bool approx_ok = real && !bad && isfinite(m) && m >= 1e-18f && m <= 1e18f;
+        const uint32_t f = real ? ((bad ? kQueryNonFinite : 0u) | (approx_ok ? 0u : kQueryNoApprox)) : kQueryNoApprox;
+        nb[qi] = real ? m : 0.0f;
+        qflags[qi] = f;
+        qids[qi] = (int32_t)(real ? qi : (nq ? nq - 1 : 0));
+        if (f & kQueryNonFinite) atomicOr(status + kStQueryFlags, kQueryNonFinite);
+        s_mag = m;
+        s_flags = f;
+    }
+    __syncthreads();
+    const bool ok = !(s_flags & kQueryNoApprox);
+    if (!with_op) return;
+    auto val = [&](uint32_t c) -> float { return staged ? row[c] : dst[c]; };
+    if (op == kFilterBF16) {
+        uint16_t* o = static_cast<uint16_t*>(qop) + (uint64_t)qi * ld;
+        const float m = ok ? s_mag : 1.0f;
+        for (uint32_t c = lane; c < ld; c += kWave)
+            o[c] = (ok && c < dim) ? f32_to_bf16_rne(val(c) / m) : (uint16_t)0;
+        if (lane == 0) ebound[qi] = ok ? (float)kEBoundBF16 : INFINITY;
+        return;
+    }
+    int8_t* o = static_cast<int8_t*>(qop) + (uint64_t)qi * ld;
     double ss = 0.0, mx = 0.0;
     if (ok) {
         for (uint32_t c = lane; c < dim; c += kWave) {
-            const double x = b[c];
+            const double x = val(c);
             ss += x * x;
             mx = fmax(mx, fabs(x));
         }
@@ -320,7 +311,7 @@ __global__ __launch_bounds__(64) void k_query_i8(const float* __restrict__ qf32,
             for (int j = 0; j < 4; ++j) {
                 const uint32_t c = c0 + j;
                 if (c < dim) {
-                    const double x = (double)b[c] * inv;
+                    const double x = (double)val(c) * inv;
                     qv[j] = quant_i8(x, s);
                     const double d = x - s * (double)qv[j];
                     e2 += d * d;
@@ -387,14 +378,8 @@ hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint
     return hipGetLastError();
 }
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_query_norms, dim3((a.qpad + 63) / 64), dim3(64), 0, s, a.q, a.nq, a.qpad, a.dim, a.op,
-                       a.nb, a.ebound, a.qflags, a.status);
-    hipLaunchKernelGGL(k_query_convert, dim3(grid_for((uint64_t)a.qpad * a.ld, 256)), dim3(256), 0, s, a.q, a.nq,
-                       a.qpad, a.dim, a.ld, a.nb, a.qflags, a.qf32,
-                       a.op == kFilterBF16 ? static_cast<uint16_t*>(a.qop) : nullptr);
-    if (a.op == kFilterI8)
-        hipLaunchKernelGGL(k_query_i8, dim3(a.qpad), dim3(64), 0, s, a.qf32, a.nq, a.dim, a.ld, a.qflags, a.ea_max,
-                           static_cast<int8_t*>(a.qop), a.qscale, a.ebound);
+    hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(64), 0, s, a.q, a.nq, a.dim, a.ld, a.op, a.with_op,
+                       a.ea_max, a.qf32, a.nb, a.qop, a.qscale, a.ebound, a.qflags, a.qids, a.status);
     return hipGetLastError();
 }
 

@@ -66,7 +66,9 @@ struct QueryPrepArgs {
     float* qscale;         // i8: [qpad]
     float* ebound;         // [qpad]
     uint32_t* qflags;      // [qpad]
+    int32_t* qids;         // [qpad]: min(q, nq-1), the exact scan's query-id list
     uint32_t* status;      // kStQueryFlags word receives the OR of the flags
+    bool with_op;          // build the filter operand (false: exact scan only)
 };
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s);
 
@@ -91,6 +93,11 @@ struct GemmArgs {
 };
 hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s);
 hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s);
+// int8 only, batches of <= 16 queries (query tile rows 0..15), HBM-bound: the same
+// contract as the two launches above.
+constexpr uint32_t kSkinnyMaxQ = 16;
+hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s);
+hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s);
 
 // tau[q] = the ks-th best sampled score; also zeroes cnt[0..qpad) and the status words
 // kStFail / kStEmitted for the emit pass that follows.
@@ -117,9 +124,10 @@ hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint6
                              uint64_t* part, hipStream_t s);
 hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t* qids,
                               uint32_t nqf, uint32_t k, uint64_t* out_keys, hipStream_t s);
+// Keys -> (global index, distance) rows; also zeroes the status words for the next search.
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* out_idx, float* out_dist,
-                           uint32_t* out_count, hipStream_t s);
+                           uint32_t* out_count, uint32_t* status, hipStream_t s);
 hipError_t launch_cosine_pair(const float* a, uint32_t la, const float* b, uint32_t lb,
                               float* out, hipStream_t s);
 

@@ -79,10 +79,15 @@ def test_golden_search(bsr_mod, gpu, exact_only):
 
 
 # ---- exact scan (small batches) and filter path (batches) vs the oracle --------------
+FILTERS = pytest.mark.parametrize("fflags", [0, 4], ids=["i8", "bf16"])  # 4 = BSR_FLAG_FILTER_BF16
+
+
+# ---- small batches: int8 skinny filter (bf16 index / k > 200: exact scan) vs the oracle --
+@FILTERS
 @pytest.mark.parametrize("n,dim,nq,k", [
     (1, 768, 1, 10), (5, 768, 3, 10), (257, 768, 2, 1), (1000, 768, 5, 64), (3000, 130, 9, 100),
-    (4097, 768, 4, 256), (20000, 768, 8, 50)])
-def test_exact_scan_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
+    (4097, 768, 4, 256), (20000, 768, 8, 50), (100000, 768, 16, 10), (70000, 96, 1, 10)])
+def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
     rng = np.random.default_rng(n + dim + k)
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
     if n > 10:
@@ -90,13 +95,14 @@ def test_exact_scan_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
         rows[3] = 0
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
     qs[0] = rows[min(1, n - 1)]
-    ix = _index(bsr_mod, rows)
+    ix = _index(bsr_mod, rows, flags=fflags)
     got = ix.local_top_k(qs, k)
-    assert ix.last_stats().n_exact_direct == nq
+    st = ix.last_stats()
+    if (fflags and nq < 16) or k > 200:
+        assert st.n_exact_direct == nq
+    else:
+        assert st.n_exact_direct == 0 and st.n_fallback == 0, (st.n_exact_direct, st.n_fallback)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
-
-
-FILTERS = pytest.mark.parametrize("fflags", [0, 4], ids=["i8", "bf16"])  # 4 = BSR_FLAG_FILTER_BF16
 
 
 @FILTERS

@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes over the filter microbenchmark (tooling).  Each pass is its own rocprofv3 run
+# (counters only with --kernel-trace-free --pmc; never combined with trace domains).
+# usage: bash tools/microbench/pmc_filter.sh OUTDIR
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 9
+export TMPDIR=/tmp
+B=./tools/microbench/gemm_ablate
+O=${1:-gpurun_out/pmc_filter}
+mkdir -p "$O"
+i=0
+for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+            "SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU" \
+            "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $pass -d "$O/p$i" -o run --output-format csv -- $B 1000000 1000 3 > "$O/p$i.log" 2>&1
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python3 tools/microbench/pmc_summary.py "$O" > "$O/summary.txt"; cat "$O/summary.txt"
