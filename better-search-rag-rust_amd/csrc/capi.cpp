@@ -24,6 +24,8 @@ int bsr_index_get_many_impl(const bsr_index* ix, uint64_t offset, uint64_t count
 int bsr_local_top_k_impl(bsr_index* ix, const float* queries, uint32_t nq, uint32_t k, uint64_t* out_idx,
                          float* out_dist, uint32_t* out_count);
 int bsr_index_collect_profile_impl(bsr_index* ix);
+int bsr_copy_out_impl(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx, float* out_dist,
+                      uint32_t* out_count);
 
 #define BSR_GUARD(expr)                                                        \
     try {                                                                      \
@@ -362,17 +364,13 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     if (!nq) return BSR_OK;
     const size_t nk = (size_t)nq * k;
     if (single) {
-        BSR_HIP(hipMemcpyAsync(out_idx, ix->o_idx.p, nk * sizeof(uint64_t), hipMemcpyDefault, ix->stream));
-        BSR_HIP(hipMemcpyAsync(out_dist, ix->o_dist.p, nk * sizeof(float), hipMemcpyDefault, ix->stream));
-        BSR_HIP(hipMemcpyAsync(out_count, ix->o_cnt.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, ix->stream));
-        BSR_HIP(hipStreamSynchronize(ix->stream));
+        BSR_TRY(bsr_copy_out_impl(ix, nq, k, out_idx, out_dist, out_count));
         bsr_index_collect_profile_impl(ix);
         return BSR_OK;
     }
     // gather_top_k_results (:194) as an RCCL all-gather on the index's stream, then the
     // root's merge (:200-202).
-    BSR_TRY(allgather_lists(c, ix->o_idx.as<uint64_t>(), ix->o_dist.as<float>(), ix->o_cnt.as<uint32_t>(), nq, k,
-                            ix->stream));
+    BSR_TRY(allgather_lists(c, ix->d_idx, ix->d_dist, ix->d_cnt, nq, k, ix->stream));
     if (root) {
         c->h_idx.resize(nk * c->size);
         c->h_dist.resize(nk * c->size);

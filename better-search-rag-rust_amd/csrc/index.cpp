@@ -325,7 +325,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.n_qt = qpad / kFilterTile;
     g.a_scale = ix->ascale.as<float>();
     g.b_scale = ix->qscale.as<float>();
-    uint32_t* status = ix->status.as<uint32_t>();
+    uint32_t* status = ix->d_status;
 
     if (n > cap) {
         // tau0 from every 32nd row: the ks-th best sampled score, or (large shards) the
@@ -390,9 +390,35 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     stats.n_queries = nq;
     stats.filter_op = (uint32_t)op;
     stats.row_ebound = row_ebound;
-    BSR_TRY(o_idx.ensure((size_t)std::max(nq, 1u) * k * sizeof(uint64_t)));
-    BSR_TRY(o_dist.ensure((size_t)std::max(nq, 1u) * k * sizeof(float)));
-    BSR_TRY(o_cnt.ensure((size_t)std::max(nq, 1u) * sizeof(uint32_t)));
+    // packed result layout for this batch
+    const size_t nqk = (size_t)std::max(nq, 1u) * k;
+    res_off_cnt = 16;
+    res_off_dist = round_up(res_off_cnt + (size_t)std::max(nq, 1u) * sizeof(uint32_t), 16);
+    res_off_idx = round_up(res_off_dist + nqk * sizeof(float), 16);
+    res_bytes = res_off_idx + nqk * sizeof(uint64_t);
+    if (res[0].bytes < res_bytes || res[1].bytes < res_bytes) {
+        for (DevBuf& r : res) {
+            BSR_TRY(r.ensure(res_bytes));
+            BSR_HIP(hipMemsetAsync(r.p, 0, r.bytes, stream));  // status words start at zero
+        }
+        next_status_clean = true;
+    }
+    if (h_res_bytes < res_bytes) {
+        if (h_res) BSR_HIP(hipHostFree(h_res));
+        h_res = nullptr;
+        h_res_bytes = 0;
+        BSR_HIP(hipHostMalloc((void**)&h_res, res_bytes, hipHostMallocDefault));
+        h_res_bytes = res_bytes;
+    }
+    cur ^= 1u;
+    uint8_t* rb = res[cur].as<uint8_t>();
+    d_status = reinterpret_cast<uint32_t*>(rb);
+    d_cnt = reinterpret_cast<uint32_t*>(rb + res_off_cnt);
+    d_dist = reinterpret_cast<float*>(rb + res_off_dist);
+    d_idx = reinterpret_cast<uint64_t*>(rb + res_off_idx);
+    uint32_t* next_status = res[cur ^ 1u].as<uint32_t>();
+    if (!next_status_clean) BSR_HIP(hipMemsetAsync(d_status, 0, kStWords * sizeof(uint32_t), stream));
+    next_status_clean = false;
     if (nq == 0) return BSR_OK;
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
 
@@ -403,7 +429,6 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     BSR_TRY(qscale.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(ebound.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(qflags.ensure((size_t)qpad * sizeof(uint32_t)));
-    BSR_TRY(status.ensure(kStWords * sizeof(uint32_t)));
     BSR_TRY(qids_id.ensure((size_t)qpad * sizeof(int32_t)));
     BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
 
@@ -414,9 +439,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
         qsrc = q_in.as<float>();
     }
-    // status words are zeroed by the previous search's finalize kernel (or here once)
-    if (!status_clean) BSR_HIP(hipMemsetAsync(status.p, 0, kStWords * sizeof(uint32_t), stream));
-    status_clean = false;
+    // (the status words of res[cur] were zeroed by the previous search's finalize)
     // int8 indexes filter every batch (small ones with the skinny kernels); bf16 indexes
     // only batches of >= 16 queries (smaller ones take the exact scan).
     const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter &&
@@ -436,7 +459,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     qa.ebound = ebound.as<float>();
     qa.qflags = qflags.as<uint32_t>();
     qa.qids = qids_id.as<int32_t>();
-    qa.status = status.as<uint32_t>();
+    qa.status = d_status;
     qa.with_op = use_filter;
     BSR_HIP(launch_query_prep(qa, stream));
 
@@ -450,10 +473,19 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     } else {
         BSR_TRY(run_filter(ix, nq, qpad, k));
     }
-    // The one status readback of the batch: non-finite queries, uncertified queries.
-    uint32_t st[kStWords] = {0, 0, 0, 0};
-    BSR_HIP(hipMemcpyAsync(st, status.p, sizeof st, hipMemcpyDeviceToHost, stream));
-    BSR_HIP(hipStreamSynchronize(stream));
+    // Finalize into the packed result and read it back with ONE copy: status words
+    // (non-finite queries, uncertified queries) and the lists.
+    auto finalize_and_read = [&]() -> int {
+        BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
+                                stream));
+        next_status_clean = true;
+        ev_end(ix, ev_total);
+        BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
+        BSR_HIP(hipStreamSynchronize(stream));
+        return BSR_OK;
+    };
+    BSR_TRY(finalize_and_read());
+    const uint32_t* st = reinterpret_cast<const uint32_t*>(h_res);
     if (st[kStQueryFlags] & kQueryNonFinite) {
         h_qflags.resize(nq);
         BSR_HIP(hipMemcpy(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -481,25 +513,33 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
                 else ++stats.n_fallback;
             }
             BSR_TRY(run_exact_scan_list(ix, exact_ids, k));
+            BSR_TRY(finalize_and_read());
         }
     }
-    BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, o_idx.as<uint64_t>(), o_dist.as<float>(),
-                            o_cnt.as<uint32_t>(), status.as<uint32_t>(), stream));
-    status_clean = true;
-    ev_end(ix, ev_total);
     return BSR_OK;
 }
 
+// Results of the last search to the caller's arrays: from the pinned host mirror for host
+// arrays, device-to-device for device arrays.
 static int copy_out(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
     const size_t nk = (size_t)nq * k;
-    if (out_idx)
-        BSR_HIP(hipMemcpyAsync(out_idx, ix->o_idx.p, nk * sizeof(uint64_t), hipMemcpyDefault, ix->stream));
-    if (out_dist)
-        BSR_HIP(hipMemcpyAsync(out_dist, ix->o_dist.p, nk * sizeof(float), hipMemcpyDefault, ix->stream));
-    if (out_count)
-        BSR_HIP(hipMemcpyAsync(out_count, ix->o_cnt.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, ix->stream));
+    const bool dev = is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count);
+    if (!dev) {
+        if (out_idx) memcpy(out_idx, ix->h_res + ix->res_off_idx, nk * sizeof(uint64_t));
+        if (out_dist) memcpy(out_dist, ix->h_res + ix->res_off_dist, nk * sizeof(float));
+        if (out_count) memcpy(out_count, ix->h_res + ix->res_off_cnt, (size_t)nq * sizeof(uint32_t));
+        return BSR_OK;
+    }
+    if (out_idx) BSR_HIP(hipMemcpyAsync(out_idx, ix->d_idx, nk * sizeof(uint64_t), hipMemcpyDefault, ix->stream));
+    if (out_dist) BSR_HIP(hipMemcpyAsync(out_dist, ix->d_dist, nk * sizeof(float), hipMemcpyDefault, ix->stream));
+    if (out_count) BSR_HIP(hipMemcpyAsync(out_count, ix->d_cnt, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, ix->stream));
     BSR_HIP(hipStreamSynchronize(ix->stream));
     return BSR_OK;
+}
+
+int bsr_copy_out_impl(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx, float* out_dist,
+                      uint32_t* out_count) {
+    return copy_out(ix, nq, k, out_idx, out_dist, out_count);
 }
 
 static void collect_profile(bsr_index* ix) {

@@ -74,15 +74,30 @@ struct bsr_index {
     bsr::DevBuf flags;  // u32 [2]: row flags, int8 row error bound (f32 bits)
 
     // per-search scratch
-    bsr::DevBuf q_in, qf32, nb, qop, qscale, ebound, qflags, status, tau, S, cand, cnt, cand_rows,
-        ncand, tau_excl, keys, fail, part, qids, qids_id, o_idx, o_dist, o_cnt, tmp;
-    bool status_clean = false;  // status words known to be zero (finalize of the last search)
+    bsr::DevBuf q_in, qf32, nb, qop, qscale, ebound, qflags, tau, S, cand, cnt, cand_rows, ncand,
+        tau_excl, keys, fail, part, qids, qids_id, tmp;
+
+    // Packed per-search result, double-buffered: [status words | counts | distances |
+    // indices].  One D2H copy per search reads it all back (into pinned memory); the
+    // finalize kernel of search i zeroes the status words of the buffer search i+1 uses.
+    bsr::DevBuf res[2];
+    uint8_t* h_res = nullptr;  // pinned (hipHostMalloc) mirror of one result buffer
+    size_t h_res_bytes = 0;
+    uint32_t cur = 0;          // result buffer of the last search
+    bool next_status_clean = false;  // status words of res[cur ^ 1] are known to be zero
+    size_t res_off_cnt = 0, res_off_dist = 0, res_off_idx = 0, res_bytes = 0;
+    uint32_t* d_status = nullptr;
+    uint32_t* d_cnt = nullptr;
+    float* d_dist = nullptr;
+    uint64_t* d_idx = nullptr;
+    ~bsr_index() { if (h_res) (void)hipHostFree(h_res); }
     std::vector<uint32_t> h_qflags, h_fail;
 
     bsr_search_stats stats{};
     bsr_profile prof{};
     bsr::Events ev_emit, ev_sample, ev_select, ev_rescore, ev_scan, ev_total;
 
-    // Run the local search; results stay in o_idx / o_dist / o_cnt (device, [nq][k]).
+    // Run the local search; results stay in d_idx / d_dist / d_cnt (device, [nq][k]) and in
+    // the pinned host mirror h_res at the same offsets.
     int search_device(const float* queries, uint32_t nq, uint32_t k);
 };

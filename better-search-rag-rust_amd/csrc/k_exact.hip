@@ -77,7 +77,8 @@ __global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, 
                                                 uint64_t* __restrict__ out_keys,
                                                 uint32_t* __restrict__ status,
                                                 uint32_t* __restrict__ fail_list) {
-    __shared__ __attribute__((aligned(16))) float lds[64 * 68];
+    __shared__ __attribute__((aligned(16))) float lds[64 * 68 + 64];  // 64 rows + the query chunk
+    float* ldq = lds + 64 * 68;
     const uint32_t q = blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x;
@@ -96,20 +97,27 @@ __global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, 
         uint32_t lrow[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
-        f32x4_t pre[16];
-        load_cand_chunk(pre, rows, ld, lrow, 0, lane);
-        for (uint32_t ch = 0; ch < nch; ++ch) {
+        // two chunks of loads in flight (register sets A / B), one LDS stage
+        f32x4_t preA[16], preB[16];
+        load_cand_chunk(preA, rows, ld, lrow, 0, lane);
+        if (nch > 1) load_cand_chunk(preB, rows, ld, lrow, 1, lane);
+        auto step = [&](f32x4_t (&pre)[16], uint32_t ch) {
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int L16 = i * 64 + lane;
                 *reinterpret_cast<f32x4_t*>(lds + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
             }
+            ldq[lane] = bq[ch * 64 + lane];  // the query chunk (LDS broadcast reads)
             __syncthreads();
-            load_cand_chunk(pre, rows, ld, lrow, ch + 1 < nch ? ch + 1 : ch, lane);  // clamped prefetch
-            const float* const bb[1] = {bq + ch * 64};
+            if (ch + 2 < nch) load_cand_chunk(pre, rows, ld, lrow, ch + 2, lane);
+            const float* const bb[1] = {ldq};
             const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
             seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
+        };
+        for (uint32_t ch = 0; ch < nch; ch += 2) {
+            step(preA, ch);
+            if (ch + 1 < nch) step(preB, ch + 1);
         }
         const float d = finish_distance(acc[0], mx[0], na[myrow], mag_b);
         L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)k, thr);
@@ -307,7 +315,7 @@ __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint3
                            uint64_t offset, uint64_t* __restrict__ out_idx, float* __restrict__ out_dist,
                            uint32_t* __restrict__ out_count, uint32_t* __restrict__ status) {
     const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (e < kStWords) status[e] = 0;  // read back by the host before this kernel runs
+    if (e < kStWords) status[e] = 0;  // the status words of the NEXT search's result buffer
     if (e >= (uint64_t)nq * k) return;
     const uint32_t q = (uint32_t)(e / k), i = (uint32_t)(e - (uint64_t)q * k);
     const uint32_t cnt = (uint64_t)k < n ? k : (uint32_t)n;

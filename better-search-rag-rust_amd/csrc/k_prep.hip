@@ -251,22 +251,34 @@ __global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, 
     const bool staged = ld <= kQueryLdsFloats;
     const float* src = q + (uint64_t)qi * dim;
     float* dst = qf32 + (uint64_t)qi * ld;
+    bool bad = false;
     for (uint32_t c = lane; c < ld; c += kWave) {
         const float v = (real && c < dim) ? src[c] : 0.0f;
+        bad |= !isfinite(v);
         dst[c] = v;
         if (staged) row[c] = v;
     }
+    bad = __ballot(bad) != 0;
     __syncthreads();
     if (lane == 0) {
+        // the reference's sequential sum, 16 elements per step from 4 ds_read_b128
         float acc = -0.0f;
-        bool bad = false;
-        if (real) {
-            for (uint32_t i = 0; i < dim; ++i) {
-                const float x = staged ? row[i] : src[i];
-                bad = bad || !isfinite(x);
-                acc = acc + x * x;
+        uint32_t i = 0;
+        if (real && staged) {
+            const float4* r4 = reinterpret_cast<const float4*>(row);
+            for (; i + 16 <= dim; i += 16) {
+                const float4 x0 = r4[i / 4], x1 = r4[i / 4 + 1], x2 = r4[i / 4 + 2], x3 = r4[i / 4 + 3];
+                acc = acc + x0.x * x0.x; acc = acc + x0.y * x0.y; acc = acc + x0.z * x0.z; acc = acc + x0.w * x0.w;
+                acc = acc + x1.x * x1.x; acc = acc + x1.y * x1.y; acc = acc + x1.z * x1.z; acc = acc + x1.w * x1.w;
+                acc = acc + x2.x * x2.x; acc = acc + x2.y * x2.y; acc = acc + x2.z * x2.z; acc = acc + x2.w * x2.w;
+                acc = acc + x3.x * x3.x; acc = acc + x3.y * x3.y; acc = acc + x3.z * x3.z; acc = acc + x3.w * x3.w;
             }
         }
+        if (real)
+            for (; i < dim; ++i) {
+                const float x = staged ? row[i] : src[i];
+                acc = acc + x * x;
+            }
         const float m = __builtin_sqrtf(acc);
         const bool approx_ok = real && !bad && isfinite(m) && m >= 1e-18f && m <= 1e18f;
         const uint32_t f = real ? ((bad ? kQueryNonFinite : 0u) | (approx_ok ? 0u : kQueryNoApprox)) : kQueryNoApprox;

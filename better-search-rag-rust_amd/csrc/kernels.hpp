@@ -124,7 +124,8 @@ hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint6
                              uint64_t* part, hipStream_t s);
 hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t* qids,
                               uint32_t nqf, uint32_t k, uint64_t* out_keys, hipStream_t s);
-// Keys -> (global index, distance) rows; also zeroes the status words for the next search.
+// Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
+// result buffer the next search will use.
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* out_idx, float* out_dist,
                            uint32_t* out_count, uint32_t* status, hipStream_t s);
