@@ -1,11 +1,12 @@
 // Microbenchmark (tooling): the MFMA filter kernel (int8 and bf16 operands) and its
 // ablations on a synthetic shard.  Includes the product kernel source directly.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../../include -I../../better-search-rag-rust_amd/csrc gemm_ablate.hip -o gemm_ablate
-// Run: ./gemm_ablate [rows] [queries] [rounds]
+// Run: ./gemm_ablate [rows] [queries] [rounds] [variant-substring]
 #include "k_filter.hip"
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
+#include <string.h>
 
 using namespace bsr;
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -31,6 +32,7 @@ __global__ void fill_f32(float* p, size_t n, float v) {
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 1000000, nq = argc > 2 ? atoi(argv[2]) : 1000, ld = 768;
     const int rounds = argc > 3 ? atoi(argv[3]) : 6;
+    const char* only = argc > 4 ? argv[4] : nullptr;
     const uint32_t qpad = (nq + 255) / 256 * 256, npad = (n + 255) / 256 * 256;
     uint8_t *A16, *B16, *A8, *B8; float *tau, *as, *bs; uint64_t* cand; uint32_t* cnt;
     const uint32_t cap = 1024;
@@ -61,6 +63,12 @@ int main(int argc, char** argv) {
         {"i8 no-DMA", k_filter<OpI8, true, 1>, true, 1e9f, {}},
         {"i8 DMA-only", k_filter<OpI8, true, 3>, true, 1e9f, {}},
     };
+    if (only) {
+        std::vector<V> keep;
+        for (auto& v : vs)
+            if (strstr(v.name, only)) keep.push_back(v);
+        vs.swap(keep);
+    }
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
     for (int r = 0; r < rounds; ++r) {
@@ -83,6 +91,26 @@ int main(int argc, char** argv) {
                 printf("  [%s] emitted per query %.1f\n", v.name, tot / nq);
             }
         }
+    }
+    // skinny int8 filter (1 query, HBM-bound): GB/s of the int8 rows
+    if (!only || strstr("skinny", only)) {
+        GemmArgs gs = g;
+        gs.A = A8; gs.B = B8; gs.row_bytes = ld; gs.a_stride = ld;
+        std::vector<float> ht(qpad, 0.125f);
+        CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
+        std::vector<float> ts;
+        for (int r = 0; r < rounds + 1; ++r) {
+            CHECK(hipMemset(cnt, 0, qpad * 4));
+            CHECK(hipEventRecord(e0));
+            hipLaunchKernelGGL(k_filter_skinny<true>, dim3(768), dim3(256), 0, 0, gs);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 0) ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f GB/s of int8 rows at median)\n", "skinny 1-16 q",
+               ts[ts.size() / 2], ts[0], (double)n * ld / (ts[ts.size() / 2] * 1e-3) / 1e9);
     }
     for (auto& v : vs) {
         std::sort(v.t.begin(), v.t.end());
