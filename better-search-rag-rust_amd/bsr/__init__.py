@@ -14,6 +14,9 @@ reference (paths relative to nichmorgan/better-search-rag-rust):
 ``compute_global_top_k``               src/mpi_helpers/metrics.rs:141-171
 ``parallel_top_k_similarity_search``   src/mpi_helpers/metrics.rs:174-206
 ``calculate_accuracy_metrics``         src/mpi_helpers/metrics.rs:217-249
+``PolarsVectorstore`` (lib/libbsr_vstore.so, include/bsr_vstore.h)
+                                       src/vectorstore/polars.rs:7-247
+``get_global_vstore/get_local_vstore`` src/mpi_helpers/vectorstore.rs:5-20
 =====================================  ===============================================
 """
 from __future__ import annotations
@@ -27,6 +30,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr.so")
+VSTORE_LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr_vstore.so")
 
 BSR_OK = 0
 BSR_F32 = 0
@@ -98,6 +102,7 @@ def lib() -> ctypes.CDLL:
         "bsr_index_load": (ctypes.c_int, [_P, _P, u64, u64]),
         "bsr_index_append": (ctypes.c_int, [_P, _P, u64]),
         "bsr_index_count": (ctypes.c_int, [_P, ctypes.POINTER(u64)]),
+        "bsr_index_dim": (ctypes.c_int, [_P, ctypes.POINTER(u32)]),
         "bsr_index_global_offset": (ctypes.c_int, [_P, ctypes.POINTER(u64)]),
         "bsr_index_get_many": (ctypes.c_int, [_P, u64, u64, _P]),
         "bsr_local_top_k": (ctypes.c_int, [_P, _P, u32, u32, _P, _P, _P]),
@@ -441,3 +446,149 @@ def synth_uniform_np(row0: int, n_rows: int, dim: int, seed: int) -> np.ndarray:
         x = x ^ (x >> np.uint64(31))
     v = (x >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 8388608.0) - np.float32(1.0)
     return v.reshape(n_rows, dim)
+
+
+# ---- f-1: the parquet vector store (src/vectorstore/polars.rs) ------------------------------
+_vlib = None
+
+
+def vstore_lib() -> ctypes.CDLL:
+    """Load libbsr_vstore.so (Arrow C++ / Parquet; host only)."""
+    global _vlib
+    if _vlib is not None:
+        return _vlib
+    lib()  # libbsr.so first (the adapter links it and shares its error state)
+    if not os.path.exists(VSTORE_LIB_PATH):
+        raise BsrError(-3, f"{VSTORE_LIB_PATH} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(VSTORE_LIB_PATH)
+    u32, u64, i32, i64 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "bsr_vstore_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P)]),
+        "bsr_vstore_close": (None, [_P]),
+        "bsr_vstore_path": (ctypes.c_char_p, [_P]),
+        "bsr_vstore_get_count": (ctypes.c_int, [_P, ctypes.POINTER(u64)]),
+        "bsr_vstore_get_many": (ctypes.c_int, [_P, i64, u64, _P, u64, _P, u64, ctypes.POINTER(u64),
+                                               ctypes.POINTER(u64)]),
+        "bsr_vstore_read_slab": (ctypes.c_int, [_P, i64, u64, u32, _P, u64, ctypes.POINTER(u64)]),
+        "bsr_vstore_get": (ctypes.c_int, [_P, u64, _P, u32, ctypes.POINTER(u32)]),
+        "bsr_vstore_append_many": (ctypes.c_int, [_P, _P, u64, u32]),
+        "bsr_vstore_persist": (ctypes.c_int, [_P]),
+        "bsr_vstore_reload": (ctypes.c_int, [_P, ctypes.c_int]),
+        "bsr_vstore_reset": (ctypes.c_int, [_P]),
+        "bsr_vstore_global_path": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
+        "bsr_vstore_local_path": (ctypes.c_int, [ctypes.c_char_p, i32, ctypes.c_char_p, ctypes.c_size_t]),
+        "bsr_index_load_vstore": (ctypes.c_int, [_P, _P, i32, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _vlib = L
+    return L
+
+
+class PolarsVectorstore:
+    """src/vectorstore/polars.rs:7-247 over libbsr_vstore.so: one parquet file, one column
+    "embeddings" of List(Float32).  Rows come back as lists of numpy float32 arrays (the
+    reference's Vec<Vec<f32>>); `get_many_array` gives a dense [rows][dim] array."""
+
+    def __init__(self, path: str, empty: bool):
+        h = _P()
+        _check(vstore_lib().bsr_vstore_open(os.fsencode(path), 1 if empty else 0, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def path(self) -> str:
+        return vstore_lib().bsr_vstore_path(self._h).decode()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            vstore_lib().bsr_vstore_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def get_count(self) -> int:
+        n = ctypes.c_uint64(0)
+        _check(vstore_lib().bsr_vstore_get_count(self._h, ctypes.byref(n)))
+        return n.value
+
+    def _slice(self, s: Optional[SliceArgs]) -> Tuple[int, int]:
+        if s is None:
+            return 0, self.get_count()
+        return int(s.offset), int(s.length)
+
+    def get_many(self, slice_args: Optional[SliceArgs] = None) -> List[np.ndarray]:
+        off, length = self._slice(slice_args)
+        L = vstore_lib()
+        rows, floats = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(L.bsr_vstore_get_many(self._h, off, length, None, 0, None, 0, ctypes.byref(rows), ctypes.byref(floats)))
+        vals = np.empty(max(floats.value, 1), np.float32)
+        lens = np.empty(max(rows.value, 1), np.uint32)
+        _check(L.bsr_vstore_get_many(self._h, off, length, vals.ctypes.data, vals.size, lens.ctypes.data, lens.size,
+                                     ctypes.byref(rows), ctypes.byref(floats)))
+        out, pos = [], 0
+        for n in lens[:rows.value]:
+            out.append(vals[pos:pos + int(n)].copy())
+            pos += int(n)
+        return out
+
+    def get_many_array(self, slice_args: Optional[SliceArgs] = None, dim: int = 768) -> np.ndarray:
+        off, length = self._slice(slice_args)
+        cap = max(0, min(length, self.get_count()))
+        out = np.empty((max(cap, 1), dim), np.float32)
+        got = ctypes.c_uint64(0)
+        _check(vstore_lib().bsr_vstore_read_slab(self._h, off, length, dim, out.ctypes.data, cap, ctypes.byref(got)))
+        return out[:got.value]
+
+    def get(self, index: int) -> np.ndarray:
+        n = ctypes.c_uint32(0)
+        L = vstore_lib()
+        _check(L.bsr_vstore_get(self._h, index, None, 0, ctypes.byref(n)))
+        out = np.empty(max(n.value, 1), np.float32)
+        _check(L.bsr_vstore_get(self._h, index, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out[:n.value]
+
+    def append(self, vector) -> None:
+        self.append_many([vector])
+
+    def append_many(self, vectors) -> None:
+        if len(vectors) == 0:
+            return
+        a = np.ascontiguousarray(np.asarray(vectors, np.float32))
+        if a.ndim != 2:
+            raise BsrError(-6, "append_many takes equal-length rows")
+        _check(vstore_lib().bsr_vstore_append_many(self._h, a.ctypes.data, a.shape[0], a.shape[1]))
+
+    def persist(self) -> None:
+        _check(vstore_lib().bsr_vstore_persist(self._h))
+
+    def reload(self, force: bool) -> None:
+        _check(vstore_lib().bsr_vstore_reload(self._h, 1 if force else 0))
+
+    def reset(self) -> None:
+        _check(vstore_lib().bsr_vstore_reset(self._h))
+
+
+def get_global_vstore(vstore_dir: str, empty: bool) -> PolarsVectorstore:
+    """src/mpi_helpers/vectorstore.rs:16-20: <dir>/global.parquet."""
+    buf = ctypes.create_string_buffer(4096)
+    _check(vstore_lib().bsr_vstore_global_path(os.fsencode(str(vstore_dir)), buf, len(buf)))
+    return PolarsVectorstore(buf.value.decode(), empty)
+
+
+def get_local_vstore(vstore_dir: str, rank: int, empty: bool) -> PolarsVectorstore:
+    """src/mpi_helpers/vectorstore.rs:5-13: <dir>/rank_{rank}.parquet."""
+    buf = ctypes.create_string_buffer(4096)
+    _check(vstore_lib().bsr_vstore_local_path(os.fsencode(str(vstore_dir)), rank, buf, len(buf)))
+    return PolarsVectorstore(buf.value.decode(), empty)
+
+
+def load_index_from_vstore(index: "Index", vstore: PolarsVectorstore, rank: int, size: int) -> None:
+    """The read half of compute_local_top_k (src/mpi_helpers/metrics.rs:23-33): this rank's
+    interval_by_rank block of the store, straight into the index's HBM shard."""
+    _check(vstore_lib().bsr_index_load_vstore(index._h, vstore._h, rank, size))

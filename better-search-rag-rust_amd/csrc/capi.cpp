@@ -203,6 +203,11 @@ int bsr_index_count(const bsr_index* ix, uint64_t* out) {
     *out = ix->loaded ? ix->n : 0;
     return BSR_OK;
 }
+int bsr_index_dim(const bsr_index* ix, uint32_t* out) {
+    if (!ix || !out) return set_error(BSR_E_INVALID, "null argument");
+    *out = ix->dim;
+    return BSR_OK;
+}
 int bsr_index_global_offset(const bsr_index* ix, uint64_t* out) {
     if (!ix || !out) return set_error(BSR_E_INVALID, "null argument");
     *out = ix->global_offset;

@@ -87,7 +87,7 @@ __device__ __forceinline__ void mid_barrier() {
 // VAR (tooling, tools/microbench): 1 = no LDS-DMA in the loop (compute ceiling),
 // 3 = LDS-DMA, waits and barriers only (operand-feed ceiling), 4 = A always the same tile.
 // ------------------------------------------------------------------------------------
-template <class Op, bool EMIT, int VAR = 0>
+template <class Op, bool EMIT, int VAR = 0, bool STAG = false>
 __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
     using frag_t = typename Op::frag_t;
     using acc_t = typename Op::acc_t;
@@ -117,38 +117,46 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
     const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
     const uint32_t J = my_rt * nk;
 
+    // LDS-DMA by buffer loads: per-lane byte offsets (VGPR) fixed for the kernel, the K
+    // slice in the scalar soffset, the row tile in the descriptor base, the LDS slot in M0
+    // (from a provably wave-uniform wave id), so one DMA costs ~2 instructions.
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t lrow[2], lchunk[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         lrow[i] = (w * 2 + i) * 16 + (lane >> 2);
         lchunk[i] = (lane & 3) ^ ((lrow[i] >> 2) & 3);
     }
-    const uint8_t* bsrc[2];
+    const __amdgpu_buffer_rsrc_t rsrc_b =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, p.n_qt * BN * p.row_bytes, 0x00020000);
+    uint32_t boff_dma[2], aoff_dma[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) bsrc[i] = p.B + (uint64_t)(qt * BN + lrow[i]) * p.row_bytes + lchunk[i] * 16;
-    const uint64_t a_lane_off[2] = {(uint64_t)lrow[0] * p.a_stride + lchunk[0] * 16,
-                                    (uint64_t)lrow[1] * p.a_stride + lchunk[1] * 16};
-    // DMA pointers of the slice being issued (slice jj+3), advanced incrementally.
+    for (int i = 0; i < 2; ++i) {
+        boff_dma[i] = (qt * BN + lrow[i]) * p.row_bytes + lchunk[i] * 16;
+        aoff_dma[i] = lrow[i] * (uint32_t)p.a_stride + lchunk[i] * 16;
+    }
+    // DMA state of the slice being issued (slice jj+3), advanced incrementally.
     uint32_t iss_ti = 0, iss_kt = 0;
-    const uint8_t* a_tile = p.A;
+    __amdgpu_buffer_rsrc_t rsrc_a = rsrc_b;
     auto set_issue_tile = [&]() {
         const uint32_t rt = VAR == 4 ? g0 : g0 + iss_ti * RG;
-        a_tile = p.A + (uint64_t)rt * BM * p.a_stride;
+        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
+                                                   BM * (uint32_t)p.a_stride, 0x00020000);
+        if (!EMIT) {  // sample pass: tail rows read the last valid row
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t r = rt * BM + lrow[i] < p.n_rows ? lrow[i] : p.n_rows - 1 - rt * BM;
+                aoff_dma[i] = r * (uint32_t)p.a_stride + lchunk[i] * 16;
+            }
+        }
     };
     auto dma_a = [&](uint32_t jj, int i) {
-        uint8_t* la = lds + (jj % kSlots) * SLOT;
-        const uint8_t* src = a_tile + a_lane_off[i] + iss_kt * kSliceB;
-        if (!EMIT) {  // sample pass: clamp tail rows to the last valid one
-            const uint32_t rt = g0 + iss_ti * RG;
-            if (rt * BM + lrow[i] >= p.n_rows)
-                src = p.A + (uint64_t)(p.n_rows - 1) * p.a_stride + lchunk[i] * 16 + iss_kt * kSliceB;
-        }
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(la + (w * 2 + i) * 1024), 16, 0, 0);
+        uint8_t* la = lds + (jj % kSlots) * SLOT + (wu * 2 + i) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma[i], iss_kt * kSliceB, 0, 0);
     };
     auto dma_b = [&](uint32_t jj, int i) {
-        uint8_t* lb = lds + (jj % kSlots) * SLOT + A_BYTES;
-        __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + iss_kt * kSliceB),
-                                         (lds_void_t*)(lb + (w * 2 + i) * 1024), 16, 0, 0);
+        uint8_t* lb = lds + (jj % kSlots) * SLOT + A_BYTES + (wu * 2 + i) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_b, (lds_void_t*)lb, 16, boff_dma[i], iss_kt * kSliceB, 0, 0);
     };
     auto issue_advance = [&]() {
         if (++iss_kt == nk) { iss_kt = 0; ++iss_ti; set_issue_tile(); }
@@ -232,15 +240,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         // reads go after the first MFMA group: hipcc puts a conservative lgkmcnt(0) in
         // front of an MFMA whose operands came from ds_read (it cannot see the barrier's
         // inline wait), which must not cover reads issued just before it.
+        // STAG: the wr=1 waves (the SIMD partners of the wr=0 waves) issue each DMA before
+        // the MFMA group instead of after it, so one partner's DMA issue overlaps the other
+        // partner's MFMAs (the per-wave DMA count before each barrier is unchanged).
+        const bool stag = STAG && wr == 1;
+        if (stag && iss) dma_a(jj + 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
         mfma4(fa0, fb0, 0);
         __builtin_amdgcn_sched_barrier(0);
         read_frags(jj, 1, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) dma_a(jj + 3, 0);
+        if (iss) { if (stag) dma_a(jj + 3, 1); else dma_a(jj + 3, 0); }
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa0, fb0, 1);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) dma_a(jj + 3, 1);
+        if (!stag && iss) dma_a(jj + 3, 1);
         if constexpr (kScaleDMA) {
             // this wave's 4 block scales of the current tile (rows rt*256 + wr*128 + 32m);
             // younger than every slice DMA in flight, so covered two mid-barriers later
@@ -261,15 +275,18 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
             mid_barrier<0>();
         }
         // ---- second half: kk = 1 MFMAs, next slice's kk = 0 reads, B-half DMA
+        if (stag && iss) dma_b(jj + 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
         mfma4(fa1, fb1, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (jj + 1 < J) read_frags(jj + 1, 0, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) dma_b(jj + 3, 0);
+        if (iss) { if (stag) dma_b(jj + 3, 1); else dma_b(jj + 3, 0); }
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa1, fb1, 1);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) { dma_b(jj + 3, 1); issue_advance(); }
+        if (!stag && iss) dma_b(jj + 3, 1);
+        if (iss) issue_advance();
         __builtin_amdgcn_sched_barrier(0);
 
         if (kt == nk - 1) {

@@ -124,6 +124,7 @@ int bsr_index_load(bsr_index* ix, const void* rows, uint64_t n_rows, uint64_t gl
 /* Append rows after the current ones (PolarsVectorstore::append_many, polars.rs:101-119). */
 int bsr_index_append(bsr_index* ix, const void* rows, uint64_t n_rows);
 int bsr_index_count(const bsr_index* ix, uint64_t* out);                /* get_count */
+int bsr_index_dim(const bsr_index* ix, uint32_t* out);                  /* row length */
 int bsr_index_global_offset(const bsr_index* ix, uint64_t* out);
 /* Copy `count` rows starting at local row `offset` into out (f32, host or device):
  * PolarsVectorstore::get_many(SliceArgs{offset,length}) / get (polars.rs:121-169). */

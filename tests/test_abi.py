@@ -12,8 +12,8 @@ import pytest
 from conftest import GOLDEN, ROOT
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "bsr.h")).read()
+def header_functions(header="bsr.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(bsr_[a-z_0-9]+)\s*\(", src, flags=re.M)
     return sorted(set(names))
@@ -28,6 +28,14 @@ def test_header_parsed():
 def test_library_exports_every_declared_symbol(bsr_mod):
     lib = ctypes.CDLL(bsr_mod.LIB_PATH)
     missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_vstore_library_exports_every_declared_symbol(bsr_mod):
+    lib = bsr_mod.vstore_lib()
+    names = header_functions("bsr_vstore.h")
+    assert "bsr_index_load_vstore" in names and len(names) >= 14
+    missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
 
 
