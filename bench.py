@@ -44,7 +44,17 @@ def parse():
     ap.add_argument("--filter", choices=["i8", "bf16"], default="i8",
                     help="MFMA candidate-filter operand type (results are exact either way)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
+                    help="BASELINE.json configs: c2 = 1M f32 rows/GPU, 1000 queries, top-10 (the "
+                         "headline line); c4 = 10M rows, single queries, top-10 (p50 path); c5 = the "
+                         "per-GPU shard of 50M bf16 rows over 8 GPUs (6.25M), 4096 queries, top-100")
+    a = ap.parse_args()
+    if a.config == "c4":
+        a.rows_per_gpu, a.queries, a.k = 10_000_000, 1, 10
+        a.p50_iters = max(a.p50_iters, 100)
+    elif a.config == "c5":
+        a.rows_per_gpu, a.queries, a.k = 6_250_000, 4096, 100
+    return a
 
 
 def main():
@@ -74,12 +84,17 @@ def main():
     iv = bsr.interval_by_rank(rank, world, n_total)
     start, n_local = iv.start_index, iv.get_count()
 
-    # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index.
+    # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index
+    # (config 5: rounded to a bf16 corpus first; parity is on the widened bf16 values).
     fflag = bsr.BSR_FLAG_FILTER_BF16 if args.filter == "bf16" else 0
-    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE | fflag)
+    corpus_bf16 = args.config == "c5"
+    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE | fflag,
+                      dtype=bsr.BSR_BF16 if corpus_bf16 else bsr.BSR_F32)
     shard = torch.empty((max(n_local, 1), D), dtype=torch.float32, device=dev)
     if n_local:
         bsr.synth_uniform(shard.data_ptr(), start, n_local, D, 42)
+    if corpus_bf16:
+        shard = shard.to(torch.bfloat16)
     torch.cuda.synchronize()
     index.load(shard[:n_local] if n_local else np.zeros((0, D), np.float32), start)
     del shard
@@ -159,7 +174,7 @@ def main():
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        value = Q * world / (ms_per_step * 1e-3)
+        value = (Q * world if args.config == "c2" else Q) / (ms_per_step * 1e-3)
         out = {
             "metric": "queries/sec + p50 latency, 768-d top-10 over N vectors @1/2/4/8 GPU",
             "value": round(value, 2),
@@ -172,10 +187,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.filter,
-            "data": "synthetic U(-1,1) f32 corpus generated on device (seed 42), 1000 queries (seed 43, query 0 = row 0)",
+            "data": f"synthetic U(-1,1) {'bf16' if corpus_bf16 else 'f32'} corpus generated on device (seed 42), "
+                    f"{Q} queries (seed 43, query 0 = row 0)",
             "config": {
-                "workload": f"configs[1] per GPU: {n_local} x {D} f32 rows per GPU ({n_total} total), "
-                            f"{Q} batched queries, top-{K}; value = queries x 1M-row shards / s",
+                "workload": {"c2": "configs[1] per GPU", "c4": "configs[3] (single-query path)",
+                             "c5": "configs[4] per-GPU shard"}[args.config] +
+                            f": {n_local} x {D} {'bf16' if corpus_bf16 else 'f32'} rows per GPU ({n_total} total), "
+                            f"{Q} batched queries, top-{K}" +
+                            ("; value = queries x 1M-row shards / s" if args.config == "c2" else "; value = queries / s"),
                 "rows_total": n_total, "rows_per_gpu": n_local, "queries": Q, "top_k": K, "dim": D,
                 "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank) + RCCL all-gather",
                 "filter": ("int8 MFMA (v_mfma_i32_32x32x32_i8) candidates" if args.filter == "i8" else

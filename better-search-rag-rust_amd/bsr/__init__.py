@@ -62,7 +62,7 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("n_queries", ctypes.c_uint32), ("n_exact_direct", ctypes.c_uint32),
                 ("n_fallback", ctypes.c_uint32), ("n_candidates", ctypes.c_uint32),
                 ("n_emitted", ctypes.c_uint64), ("filter_op", ctypes.c_uint32),
-                ("row_ebound", ctypes.c_float)]
+                ("row_ebound", ctypes.c_float), ("n_rescued", ctypes.c_uint32)]
 
 
 class Profile(ctypes.Structure):
@@ -231,6 +231,11 @@ class Index:
                 raise BsrError(-6, f"row length {rows.shape[1]} != dim {self.dim}")
             return rows, n
         n = int(rows.shape[0]) if rows.dim() > 1 else 1
+        want = 2 if self.dtype == BSR_BF16 else 4
+        if rows.element_size() != want or not rows.is_contiguous():
+            raise BsrError(-1, f"rows must be a contiguous {want}-byte tensor for this index dtype")
+        if n and int(rows.shape[-1]) != self.dim:
+            raise BsrError(-6, f"row length {int(rows.shape[-1])} != dim {self.dim}")
         return rows, n
 
     def load(self, rows, global_offset: int = 0):

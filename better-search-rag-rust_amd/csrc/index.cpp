@@ -300,11 +300,17 @@ static int run_exact_scan_list(bsr_index* ix, const std::vector<int32_t>& ids, u
     return run_exact_scan(ix, ix->qids.as<int32_t>(), (uint32_t)ids.size(), k);
 }
 
+static uint32_t kp_for(uint32_t k) { return 64u * ((3u * k + 34u + 63u) / 64u) - 1u; }
+static uint32_t cap_for(uint32_t k) { return 16u * (kp_for(k) + 1u); }
+
 // Candidate stage (steps 2-5) for every query of the batch.  Batches of at most 16
 // queries on an int8 index use the skinny (HBM-bound, no LDS) filter kernels.
 static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     const bool skinny = ix->op == kFilterI8 && nq <= kSkinnyMaxQ;
-    const uint32_t kp = 64u * ((k + 54u + 63u) / 64u) - 1u;  // k' candidates, (k'+1) % 64 == 0
+    // k' candidates, (k'+1) % 64 == 0, about 3k: the k-th exact score must clear the (k'+1)-th
+    // approximate one by E_q, and in a Gaussian-like tail that takes ~3x as many rows at
+    // E_q/sigma ~ 0.26.  63 for k <= 10, 191 for k = 50, 383 for k = 100.
+    const uint32_t kp = kp_for(k);
     const uint32_t cap = 16u * (kp + 1u);
     const uint32_t ks = (kp + 1u) / 8u;
     const uint32_t BM = kFilterTile;
@@ -317,6 +323,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     BSR_TRY(ix->ncand.ensure((size_t)nq * sizeof(uint32_t)));
     BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));
     BSR_TRY(ix->fail.ensure((size_t)nq * sizeof(uint32_t)));
+    BSR_TRY(ix->fail2.ensure((size_t)nq * sizeof(uint32_t)));
 
     GemmArgs g{};
     g.A = ix->fop.as<uint8_t>();
@@ -373,10 +380,24 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
                                status, ix->stream));
     ev_end(ix, ix->ev_select);
     ev_begin(ix, ix->ev_rescore);
-    BSR_HIP(launch_rescore(ix->rows.as<float>(), ix->ld, ix->dim, ix->na.as<float>(), ix->qf32.as<float>(),
-                           ix->nb.as<float>(), nq, ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), kp,
-                           ix->tau_excl.as<float>(), k, ix->ebound.as<float>(), ix->keys.as<uint64_t>(), status,
-                           ix->fail.as<uint32_t>(), ix->stream));
+    RescoreArgs ra{};
+    ra.rows = ix->rows.as<float>();
+    ra.ld = ix->ld;
+    ra.dim = ix->dim;
+    ra.na = ix->na.as<float>();
+    ra.qf32 = ix->qf32.as<float>();
+    ra.nb = ix->nb.as<float>();
+    ra.n_items = nq;
+    ra.cand_rows = ix->cand_rows.as<uint32_t>();
+    ra.ncand = ix->ncand.as<uint32_t>();
+    ra.kp = kp;
+    ra.tau_excl = ix->tau_excl.as<float>();
+    ra.k = k;
+    ra.ebound = ix->ebound.as<float>();
+    ra.out_keys = ix->keys.as<uint64_t>();
+    ra.fail_cnt = status + kStFail;
+    ra.fail_list = ix->fail.as<uint32_t>();
+    BSR_HIP(launch_rescore(ra, ix->stream));
     ev_end(ix, ix->ev_rescore);
     return BSR_OK;
 }
@@ -495,13 +516,44 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     }
     if (use_filter) {
         stats.n_emitted = st[kStEmitted];
-        const uint32_t nfail = st[kStFail];
+        uint32_t nfail = st[kStFail];
+        const uint32_t* fail_dev = fail.as<uint32_t>();
+        if (nfail) {
+            // Second chance: an uncertified query rescored over EVERY row it emitted
+            // (certified against the emission threshold tau0) -- ~4k' rows instead of a scan.
+            RescoreArgs ra{};
+            ra.rows = rows.as<float>();
+            ra.ld = ld;
+            ra.dim = dim;
+            ra.na = na.as<float>();
+            ra.qf32 = qf32.as<float>();
+            ra.nb = nb.as<float>();
+            ra.n_items = nfail;
+            ra.qlist = fail.as<uint32_t>();
+            ra.cand_keys = cand.as<uint64_t>();
+            ra.cnt = cnt.as<uint32_t>();
+            ra.cap = cap_for(k);
+            ra.tau0 = tau.as<float>();
+            ra.k = k;
+            ra.ebound = ebound.as<float>();
+            ra.out_keys = keys.as<uint64_t>();
+            ra.fail_cnt = d_status + kStFail2;
+            ra.fail_list = fail2.as<uint32_t>();
+            ev_begin(ix, ev_rescore);
+            BSR_HIP(launch_rescore(ra, stream));
+            ev_end(ix, ev_rescore);
+            stats.n_rescued = nfail;
+            BSR_TRY(finalize_and_read());
+            nfail = st[kStFail2];
+            stats.n_rescued -= nfail;
+            fail_dev = fail2.as<uint32_t>();
+        }
         if (nfail) {
             // Uncertified queries, and queries the filter cannot serve (zero/tiny/huge |b|),
             // take the exact full scan: the reference's arithmetic on every row.
             h_fail.resize(nfail);
             h_qflags.resize(nq);
-            BSR_HIP(hipMemcpyAsync(h_fail.data(), fail.p, (size_t)nfail * sizeof(uint32_t), hipMemcpyDeviceToHost,
+            BSR_HIP(hipMemcpyAsync(h_fail.data(), fail_dev, (size_t)nfail * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    stream));
             BSR_HIP(hipMemcpyAsync(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    stream));

@@ -67,32 +67,28 @@ __device__ __forceinline__ void seq_chunk(const float* __restrict__ my, const fl
 }
 
 template <int E>
-__global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, uint32_t ld, uint32_t dim,
-                                                const float* __restrict__ na, const float* __restrict__ qf32,
-                                                const float* __restrict__ nb, uint32_t nq,
-                                                const uint32_t* __restrict__ cand_rows,
-                                                const uint32_t* __restrict__ ncand, uint32_t kp,
-                                                const float* __restrict__ tau_excl, uint32_t k,
-                                                const float* __restrict__ ebound_q,
-                                                uint64_t* __restrict__ out_keys,
-                                                uint32_t* __restrict__ status,
-                                                uint32_t* __restrict__ fail_list) {
+__global__ __launch_bounds__(64) void k_rescore(RescoreArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[64 * 68 + 64];  // 64 rows + the query chunk
     float* ldq = lds + 64 * 68;
-    const uint32_t q = blockIdx.x;
-    if (q >= nq) return;
+    if (blockIdx.x >= a.n_items) return;
+    const uint32_t q = a.qlist ? a.qlist[blockIdx.x] : blockIdx.x;
     const int lane = threadIdx.x;
-    const uint32_t c = ncand[q];
-    const float* bq = qf32 + (uint64_t)q * ld;
-    const float mag_b = nb[q];
-    const uint32_t nch = ld / 64;
+    // mode B (every emitted candidate) or mode A (the k' selected ones)
+    const bool all = a.cand_keys != nullptr;
+    const uint32_t cnt = all ? a.cnt[q] : a.ncand[q];
+    const bool overflow = all && cnt > a.cap;  // rows were dropped: nothing can be certified
+    const uint32_t c = overflow ? 0u : cnt;
+    const float* bq = a.qf32 + (uint64_t)q * a.ld;
+    const float mag_b = a.nb[q];
+    const uint32_t ld = a.ld, dim = a.dim, nch = ld / 64;
+    const float* rows = a.rows;
 
     WaveTopK<E> L;
     L.init();
     uint64_t thr = kKeyNone;
     for (uint32_t base = 0; base < c; base += kWave) {
-        const uint32_t ci = base + lane;
-        const uint32_t myrow = cand_rows[(uint64_t)q * kp + (ci < c ? ci : 0)];
+        const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
+        const uint32_t myrow = all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc]) : a.cand_rows[(uint64_t)q * a.kp + cc];
         float acc[1] = {-0.0f}, mx[1] = {0.0f};
         uint32_t lrow[16];
 #pragma unroll
@@ -119,18 +115,19 @@ __global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, 
             step(preA, ch);
             if (ch + 1 < nch) step(preB, ch + 1);
         }
-        const float d = finish_distance(acc[0], mx[0], na[myrow], mag_b);
-        L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)k, thr);
+        const float d = finish_distance(acc[0], mx[0], a.na[myrow], mag_b);
+        L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
     }
-    L.store(out_keys + (uint64_t)q * k, (int)k);
+    L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
 
     if (lane == 0) {
         // Certification: every row outside the candidate set has approximate
         // cosine <= tau_x, hence reference cosine <= tau_x + E_q and reference distance
         // >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must lie strictly below
-        // that, and no excluded row can be element-wise identical to the query.
-        const float tx = tau_excl[q];
-        const double ebound = (double)ebound_q[q];
+        // that, and no excluded row can be element-wise identical to the query.  Mode B:
+        // every emitted row is a candidate, so tau_x is the emission threshold tau0.
+        const float tx = overflow ? INFINITY : (all ? a.tau0[q] : a.tau_excl[q]);
+        const double ebound = (double)a.ebound[q];
         bool ok;
         if (tx == -INFINITY) {
             ok = true;  // every row of the shard was a candidate
@@ -142,8 +139,8 @@ __global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ rows, 
                  (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
         }
         if (!ok) {
-            const uint32_t pos = atomicAdd(status + kStFail, 1u);
-            fail_list[pos] = q;
+            const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
+            a.fail_list[pos] = q;
         }
     }
 }
@@ -349,22 +346,16 @@ __global__ void k_cosine_pair(const float* __restrict__ a, uint32_t la, const fl
 // ------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------
-hipError_t launch_rescore(const float* rows, uint32_t ld, uint32_t dim, const float* na, const float* qf32,
-                          const float* nb, uint32_t nq, const uint32_t* cand_rows, const uint32_t* ncand,
-                          uint32_t kp, const float* tau_excl, uint32_t k, const float* ebound, uint64_t* out_keys,
-                          uint32_t* status, uint32_t* fail_list, hipStream_t s) {
-    const uint32_t e = (k + 63) / 64;
-#define BSR_RESCORE(E)                                                                              \
-    hipLaunchKernelGGL(k_rescore<E>, dim3(nq), dim3(64), 0, s, rows, ld, dim, na, qf32, nb, nq,   \
-                       cand_rows, ncand, kp, tau_excl, k, ebound, out_keys, status, fail_list)
+hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
+    if (!a.n_items) return hipSuccess;
+    const uint32_t e = (a.k + 63) / 64;
     switch (e) {
-        case 1: BSR_RESCORE(1); break;
-        case 2: BSR_RESCORE(2); break;
-        case 3: BSR_RESCORE(3); break;
-        case 4: BSR_RESCORE(4); break;
+        case 1: hipLaunchKernelGGL(k_rescore<1>, dim3(a.n_items), dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_rescore<2>, dim3(a.n_items), dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_rescore<3>, dim3(a.n_items), dim3(64), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_rescore<4>, dim3(a.n_items), dim3(64), 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
-#undef BSR_RESCORE
     return hipGetLastError();
 }
 

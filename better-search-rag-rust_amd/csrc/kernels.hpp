@@ -31,7 +31,7 @@ constexpr uint32_t kQueryNonFinite = 1u;
 constexpr uint32_t kQueryNoApprox = 2u;   // norm zero/tiny/huge: answered by the exact scan
 
 // Search status words (device, one small D2H copy per search).
-enum StatusWord : uint32_t { kStFail = 0, kStEmitted = 1, kStQueryFlags = 2, kStWords = 4 };
+enum StatusWord : uint32_t { kStFail = 0, kStEmitted = 1, kStQueryFlags = 2, kStFail2 = 3, kStWords = 4 };
 
 // Certification bound of the bf16 filter.
 constexpr double kEBoundBF16 = 8.5e-3;
@@ -110,12 +110,33 @@ hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_
                               hipStream_t s);
 
 // ---- exact arithmetic (k_exact.hip) ---------------------------------------------------
-hipError_t launch_rescore(const float* rows, uint32_t ld, uint32_t dim, const float* na,
-                          const float* qf32, const float* nb, uint32_t nq,
-                          const uint32_t* cand_rows, const uint32_t* ncand, uint32_t kp,
-                          const float* tau_excl, uint32_t k, const float* ebound,
-                          uint64_t* out_keys, uint32_t* status, uint32_t* fail_list,
-                          hipStream_t s);
+// Exact rescoring of candidates + certification, one wave per listed query.
+struct RescoreArgs {
+    const float* rows;          // f32 [n_pad][ld]
+    uint32_t ld, dim;
+    const float* na;            // row magnitudes
+    const float* qf32;          // queries [qpad][ld]
+    const float* nb;            // query magnitudes
+    uint32_t n_items;           // queries to process (the grid)
+    const uint32_t* qlist;      // query id of item b (nullptr: b)
+    // mode A, the k' selected candidates: cand_rows[q*kp + i], i < ncand[q]; tau_excl[q]
+    const uint32_t* cand_rows;
+    const uint32_t* ncand;
+    uint32_t kp;
+    const float* tau_excl;
+    // mode B (cand_keys != nullptr), every emitted candidate: key_row(cand_keys[q*cap + i]),
+    // i < cnt[q] <= cap (an overflowed list fails); certified against tau0[q]
+    const uint64_t* cand_keys;
+    const uint32_t* cnt;
+    uint32_t cap;
+    const float* tau0;
+    uint32_t k;
+    const float* ebound;        // per-query certification bound E_q
+    uint64_t* out_keys;         // [nq][k]
+    uint32_t* fail_cnt;         // uncertified queries: count (a status word) and list
+    uint32_t* fail_list;
+};
+hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s);
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold
 // grid * kScanQF * k keys.
 hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint64_t n,

@@ -88,6 +88,7 @@ typedef struct {
     uint64_t n_emitted;        /* candidates emitted by the MFMA filter (all queries) */
     uint32_t filter_op;        /* 0 = int8 filter, 1 = bf16 filter (BSR_FLAG_FILTER_BF16) */
     float row_ebound;          /* int8: max over rows of ||a/|a| - s q||_2 (0 for bf16) */
+    uint32_t n_rescued;        /* queries certified by the second chance (all emitted rows) */
 } bsr_search_stats;
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts

@@ -152,6 +152,20 @@ def test_filter_certifies_uniform_data(bsr_mod, oracle_mod, gpu, fflags):
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "uniform")
 
 
+def test_large_k_certifies_without_fallback(bsr_mod, oracle_mod, gpu):
+    # k = 100 over a large shard (config 5's k): k' ~ 3k candidates must certify every
+    # independent query (k' = k + 54 failed them all at 6.25M rows).
+    rng = np.random.default_rng(21)
+    rows = rng.uniform(-1, 1, (300000, 768)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (24, 768)).astype(np.float32)
+    qs[0] = rows[4242]
+    ix = _index(bsr_mod, rows, max_k=100)
+    got = ix.local_top_k(qs, 100)
+    st = ix.last_stats()
+    assert st.n_fallback == 0 and st.n_candidates == 383, (st.n_fallback, st.n_rescued, st.n_candidates)
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 100), "k=100")
+
+
 @FILTERS
 def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu, fflags):
     # Clustered embeddings (dense neighbourhoods) stress the certification; any query it

@@ -59,8 +59,8 @@ int main(int argc, char** argv) {
         {"bf16 no-DMA", k_filter<OpBF16, true, 1>, false, 1e9f, {}},
         {"bf16 DMA-only", k_filter<OpBF16, true, 3>, false, 1e9f, {}},
         {"i8 tau=inf", k_filter<OpI8, true, 0>, true, 1e9f, {}},
-        {"i8 nostag tau=inf", k_filter<OpI8, true, 0, false>, true, 1e9f, {}},
-        {"i8 nostag tau=0.125", k_filter<OpI8, true, 0, false>, true, 0.125f, {}},
+        {"i8 noprio tau=inf", k_filter<OpI8, true, 0, false, false>, true, 1e9f, {}},
+        {"i8 noprio tau=0.125", k_filter<OpI8, true, 0, false, false>, true, 0.125f, {}},
         {"i8 tau=0.125", k_filter<OpI8, true, 0>, true, 0.125f, {}},
         {"i8 no-DMA", k_filter<OpI8, true, 1>, true, 1e9f, {}},
         {"i8 DMA-only", k_filter<OpI8, true, 3>, true, 1e9f, {}},
