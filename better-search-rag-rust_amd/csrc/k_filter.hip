@@ -17,6 +17,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace bsr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -491,6 +493,105 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------
+// Skinny filter v2 (dims <= 16 K steps = 1024 int8 per row): the query fragments of all K
+// steps stay in registers, and each wave walks 16-row units with the NEXT unit's A
+// fragments (one 16-byte load per K step per lane) in flight while the current unit's
+// MFMAs and epilogue run.  EMIT: units dealt round-robin over all waves (small tail).
+// SAMPLE: a wave takes the two units of one 32-sampled-row block back to back, so the
+// compact maximum over 32 sampled rows stays in a register.
+// ------------------------------------------------------------------------------------
+template <bool EMIT, int NK>
+__global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t q = lane & 15, h = lane >> 4;
+    const uint32_t nk = p.row_bytes / kSliceB;
+    const uint32_t n_units = (p.n_rows + 15) / 16;
+    const uint32_t nwaves = gridDim.x * 4, wid = blockIdx.x * 4 + w;
+    const float sbq = p.b_scale[q];
+    const float tauq = EMIT ? p.tau[q] : 0.0f;
+    i32x4_t fb[NK];
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+        fb[s] = s < (int)nk ? *reinterpret_cast<const i32x4_t*>(p.B + (uint64_t)q * p.row_bytes + h * 16 + s * kSliceB)
+                            : i32x4_t{0, 0, 0, 0};
+    // unit sequence of this wave: EMIT u = wid + i*nwaves; SAMPLE u = 2(wid + j*nwaves) + (i&1)
+    auto unit_of = [&](uint32_t i) -> uint32_t {
+        return EMIT ? wid + i * nwaves : 2 * (wid + (i >> 1) * nwaves) + (i & 1);
+    };
+    auto load = [&](i32x4_t (&fa)[NK], uint32_t u) {
+        uint32_t r = u * 16 + q;
+        r = r < p.n_rows ? r : p.n_rows - 1;  // tail rows: clamped, never emitted
+        const uint8_t* a = p.A + (uint64_t)r * p.a_stride + h * 16;
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+            if (s < (int)nk) fa[s] = *reinterpret_cast<const i32x4_t*>(a + s * kSliceB);
+    };
+    float smax = -INFINITY;  // SAMPLE compact: running maximum of the 32-row block
+    auto process = [&](const i32x4_t (&fa)[NK], uint32_t u) {
+        i32x4_acc_t acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+            if (s < (int)nk) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
+        // register i: tile row u*16 + 4h + i, query q
+        if constexpr (EMIT) {
+            const float sc = p.a_scale[(u * 16) / kQuantBlock];
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = ((float)acc[i] * sc) * sbq;
+            const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+            if (__ballot(mx >= tauq)) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t row = u * 16 + 4 * h + i;
+                    if (v[i] >= tauq && row < p.n_rows) {
+                        const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                        if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v[i], row);
+                    }
+                }
+            }
+        } else {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t tr = u * 16 + 4 * h + i;
+                tr = tr < p.n_rows ? tr : p.n_rows - 1;
+                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                v[i] = ((float)acc[i] * sc) * sbq;
+            }
+            float* srow = p.S + (uint64_t)q * p.s_ld;
+            if (!p.s_compact) {
+                *reinterpret_cast<float4*>(srow + u * 16 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+                float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+                mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+                mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                smax = fmaxf(smax, mx);
+                if ((u & 1) && h == 0) srow[u >> 1] = smax;  // second half of the block
+                if (u & 1) smax = -INFINITY;
+            }
+        }
+    };
+    // this wave's unit count
+    uint32_t n_my;
+    if (EMIT) {
+        n_my = wid < n_units ? (n_units - 1 - wid) / nwaves + 1 : 0;
+    } else {
+        const uint32_t n_blk = (n_units + 1) / 2;
+        n_my = wid < n_blk ? 2 * ((n_blk - 1 - wid) / nwaves + 1) : 0;
+    }
+    if (!n_my) return;
+    i32x4_t fa0[NK], fa1[NK];
+    load(fa0, unit_of(0));
+    for (uint32_t i = 0; i < n_my; i += 2) {
+        if (i + 1 < n_my) load(fa1, unit_of(i + 1));
+        process(fa0, unit_of(i));
+        if (i + 1 >= n_my) break;
+        if (i + 2 < n_my) load(fa0, unit_of(i + 2));
+        process(fa1, unit_of(i + 1));
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Threshold per query from the sample scores: tau0 = the ks-th largest value of S (sample
 // scores, or their maxima over 32 sampled rows -- never above the ks-th largest sample),
 // so that about ks * stride rows of the shard or more reach it.  4 waves per query.  Also
@@ -594,12 +695,25 @@ static uint32_t skinny_grid(uint32_t n_rows) {
     const uint32_t groups = (n_rows + 31) / 32, wgs = (groups + 3) / 4;
     return wgs < 768 ? (wgs ? wgs : 1) : 768;  // 3 workgroups per CU (VGPR-limited occupancy)
 }
+// v2 for rows of <= 16 K steps (1024 int8), v1 beyond.
+template <bool EMIT>
+static void launch_skinny(const GemmArgs& a, hipStream_t s) {
+    const uint32_t nk = a.row_bytes / kSliceB;
+    // v2 holds ~170 VGPRs: 2 waves per SIMD = 2 workgroups per CU
+    const uint32_t units = (a.n_rows + 15) / 16, g2 = std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
+    const dim3 g(nk <= 16 ? g2 : skinny_grid(a.n_rows)), b(256);
+    if (nk <= 4) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 4>), g, b, 0, s, a);
+    else if (nk <= 8) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 8>), g, b, 0, s, a);
+    else if (nk <= 12) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 12>), g, b, 0, s, a);
+    else if (nk <= 16) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 16>), g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_filter_skinny<EMIT>, g, b, 0, s, a);
+}
 hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_filter_skinny<false>, dim3(skinny_grid(a.n_rows)), dim3(256), 0, s, a);
+    launch_skinny<false>(a, s);
     return hipGetLastError();
 }
 hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_filter_skinny<true>, dim3(skinny_grid(a.n_rows)), dim3(256), 0, s, a);
+    launch_skinny<true>(a, s);
     return hipGetLastError();
 }
 

@@ -100,18 +100,22 @@ int main(int argc, char** argv) {
         gs.A = A8; gs.B = B8; gs.row_bytes = ld; gs.a_stride = ld;
         std::vector<float> ht(qpad, 0.125f);
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
-        std::vector<float> ts;
-        for (int r = 0; r < rounds + 1; ++r) {
+        std::vector<float> ts, ts1;
+        for (int r = 0; r < 2 * rounds + 2; ++r) {
             CHECK(hipMemset(cnt, 0, qpad * 4));
             CHECK(hipEventRecord(e0));
-            hipLaunchKernelGGL(k_filter_skinny<true>, dim3(768), dim3(256), 0, 0, gs);
+            if (r & 1) hipLaunchKernelGGL(k_filter_skinny<true>, dim3(768), dim3(256), 0, 0, gs);
+            else hipLaunchKernelGGL((k_filter_skinny2<true, 12>), dim3(512), dim3(256), 0, 0, gs);
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
             float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
-            if (r > 0) ts.push_back(ms);
+            if (r > 1) (r & 1 ? ts1 : ts).push_back(ms);
         }
         std::sort(ts.begin(), ts.end());
-        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f GB/s of int8 rows at median)\n", "skinny 1-16 q",
+        std::sort(ts1.begin(), ts1.end());
+        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f GB/s of int8 rows at median)\n", "skinny v1",
+               ts1[ts1.size() / 2], ts1[0], (double)n * ld / (ts1[ts1.size() / 2] * 1e-3) / 1e9);
+        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f GB/s of int8 rows at median)\n", "skinny v2",
                ts[ts.size() / 2], ts[0], (double)n * ld / (ts[ts.size() / 2] * 1e-3) / 1e9);
     }
     for (auto& v : vs) {
