@@ -18,6 +18,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 namespace bsr {
 
@@ -77,20 +78,35 @@ __device__ __forceinline__ void mid_barrier() {
 // The barrier sits mid-slice: the slot a DMA overwrites (slice j-1) was last read before
 // the previous barrier.  sched_barrier(0) pins the placement against the scheduler.
 //
-// Epilogue per 32x32 block (EMIT): the block maximum against the query's threshold tau
-// (one ballot), then only the passing (lane, register) pairs append (score, row) keys to
-// a per-wave LDS buffer (inline-asm ds_add_rtn; hipcc would drain vmcnt before a plain LDS
-// atomic), flushed to the per-query global lists at the end.  int8: the block scales of
+// Epilogue per 32x32 block (EMIT): the block maximum (over four group maxima of 4 rows)
+// against the query's threshold tau (one ballot); in a block that passes, only the groups
+// whose maximum passes are expanded, and their passing (lane, register) pairs append
+// (score, row) keys to a per-wave LDS buffer (inline-asm ds_add_rtn; hipcc would drain
+// vmcnt before a plain LDS atomic), flushed to the per-query global lists at the end.
+// All eight waves reach the epilogue together (the barriers keep them in step), so its
+// vector work is not hidden behind MFMAs: ~29% of the blocks pass at a realistic tau.  int8: the block scales of
 // the current tile are fetched into this wave's LDS words by a 4-lane LDS-DMA issued with
 // the tile's first slice and covered by the counted waits two slices later.
 // SAMPLE (!EMIT): every tile row is one sampled corpus row; the scores go to S, either
 // all of them (s_compact == 0) or one maximum per 32 sampled rows (s_compact == 1).
 //
+// The first MFMA group of every tile takes a zero C operand, so the accumulators are never
+// cleared by vector moves (all eight waves reach the epilogue together, so anything done
+// there is not hidden behind another wave's MFMAs).
+//
 // VAR (tooling, tools/microbench): 1 = no LDS-DMA in the loop (compute ceiling),
-// 3 = LDS-DMA, waits and barriers only (operand-feed ceiling), 4 = A always the same tile.
+// 3 = LDS-DMA, waits and barriers only (operand-feed ceiling), 4 = A always the same tile,
+// 5 = no epilogue (accumulators kept live), 6 = neither LDS-DMA nor epilogue.
+// STAMP (tooling): thread 0 of each workgroup writes its s_memtime / s_memrealtime deltas
+// to S (in-kernel clock, MI355X_MICROARCH.md 'DVFS give-back' item 6).
+// EPI (tooling): 0 = the previous epilogue (per-lane mask over all 16 registers of a block
+// whose maximum passes, explicit clears), 1 = that epilogue with zero-C first MFMAs.
 // ------------------------------------------------------------------------------------
-template <class Op, bool EMIT, int VAR = 0, bool STAG = false, bool PRIO = false>
+template <class Op, bool EMIT, int VAR = 0, bool STAG = false, bool PRIO = false, int EPI = 2, bool STAMP = false>
 __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
+    constexpr bool kNoDMA = VAR == 1 || VAR == 6, kNoMath = VAR == 3 || VAR == 4, kNoEpi = VAR == 5 || VAR == 6;
+    uint64_t t0 = 0, r0 = 0;
+    if (STAMP) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
     using frag_t = typename Op::frag_t;
     using acc_t = typename Op::acc_t;
     constexpr int BM = kFilterTile, BN = kFilterTile;
@@ -201,19 +217,27 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 
     frag_t fa0[4], fb0[2], fa1[4], fb1[2];
     auto read_frags = [&](uint32_t jj, int kk, frag_t (&fa)[4], frag_t (&fb)[2]) {
-        if constexpr (VAR >= 3) return;
-        const uint8_t* base = lds + (VAR == 1 ? 0 : jj % kSlots) * SLOT;
+        if constexpr (kNoMath) return;
+        const uint8_t* base = lds + (kNoDMA ? 0 : jj % kSlots) * SLOT;
 #pragma unroll
         for (int m = 0; m < 4; ++m) fa[m] = *reinterpret_cast<const frag_t*>(base + aoff[m][kk]);
 #pragma unroll
         for (int n = 0; n < 2; ++n) fb[n] = *reinterpret_cast<const frag_t*>(base + boff[n][kk]);
     };
-    auto mfma4 = [&](const frag_t (&fa)[4], const frag_t (&fb)[2], int half) {
-        if constexpr (VAR >= 3) return;
+    auto mfma4 = [&](const frag_t (&fa)[4], const frag_t (&fb)[2], int half, bool first) {
+        if constexpr (kNoMath) return;
+        if (EPI >= 1 && first) {  // first K step of a tile: C = 0
+            const acc_t z = {};
 #pragma unroll
-        for (int m = half * 2; m < half * 2 + 2; ++m)
+            for (int m = half * 2; m < half * 2 + 2; ++m)
 #pragma unroll
-            for (int n = 0; n < 2; ++n) acc[m][n] = Op::mfma(fa[m], fb[n], acc[m][n]);
+                for (int n = 0; n < 2; ++n) acc[m][n] = Op::mfma(fa[m], fb[n], z);
+        } else {
+#pragma unroll
+            for (int m = half * 2; m < half * 2 + 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) acc[m][n] = Op::mfma(fa[m], fb[n], acc[m][n]);
+        }
     };
     // The score of accumulator element v of block m (int8: exact integer dot, then the two
     // scale multiplies in this fixed order; the candidate keys use the same expression).
@@ -240,7 +264,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 
     uint32_t ti = 0, kt = 0;
     for (uint32_t jj = 0; jj < J; ++jj) {
-        const bool iss = VAR != 1 && jj + 3 < J;
+        const bool iss = !kNoDMA && jj + 3 < J;
         // ---- first half: kk = 0 MFMAs, kk = 1 reads, A-half DMA of slice jj+3.  The
         // reads go after the first MFMA group: hipcc puts a conservative lgkmcnt(0) in
         // front of an MFMA whose operands came from ds_read (it cannot see the barrier's
@@ -251,13 +275,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         const bool stag = STAG && wr == 1;
         if (stag && iss) dma_a(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mfma4(fa0, fb0, 0);
+        mfma4(fa0, fb0, 0, kt == 0);
         __builtin_amdgcn_sched_barrier(0);
         read_frags(jj, 1, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
         if (iss) { if (stag) dma_a(jj + 3, 1); else dma_a(jj + 3, 0); }
         __builtin_amdgcn_sched_barrier(0);
-        mfma4(fa0, fb0, 1);
+        mfma4(fa0, fb0, 1, kt == 0);
         __builtin_amdgcn_sched_barrier(0);
         if (!stag && iss) dma_a(jj + 3, 1);
         if constexpr (kScaleDMA) {
@@ -270,7 +294,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- mid-slice barrier: slice jj+1 has landed for every wave
-        if (VAR == 1) {
+        if (kNoDMA) {
             mid_barrier<8>();
         } else if (jj + 3 < J) {
             mid_barrier<6>();
@@ -282,19 +306,26 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         // ---- second half: kk = 1 MFMAs, next slice's kk = 0 reads, B-half DMA
         if (stag && iss) dma_b(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mfma4(fa1, fb1, 0);
+        mfma4(fa1, fb1, 0, false);
         __builtin_amdgcn_sched_barrier(0);
         if (jj + 1 < J) read_frags(jj + 1, 0, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
         if (iss) { if (stag) dma_b(jj + 3, 1); else dma_b(jj + 3, 0); }
         __builtin_amdgcn_sched_barrier(0);
-        mfma4(fa1, fb1, 1);
+        mfma4(fa1, fb1, 1, false);
         __builtin_amdgcn_sched_barrier(0);
         if (!stag && iss) dma_b(jj + 3, 1);
         if (iss) issue_advance();
         __builtin_amdgcn_sched_barrier(0);
 
-        if (kt == nk - 1) {
+        if (kNoEpi && kt == nk - 1) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(acc[m][n][0]));
+            kt = 0;
+            ++ti;
+        } else if (kt == nk - 1) {
             const uint32_t rt = g0 + ti * RG;
             bool stored = false;
             float sc[4] = {1.0f, 1.0f, 1.0f, 1.0f};
@@ -337,43 +368,72 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                         }
                         stored = true;
                     } else {
-                        auto mxv = acc[m][n][0];
+                        // append (score, row) to the wave's LDS buffer (inline-asm ds_add_rtn:
+                        // hipcc would drain vmcnt before a plain LDS atomic)
+                        auto emit = [&](float v, uint32_t row) {
+                            uint32_t pos;
+                            asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                                         : "=v"(pos) : "v"(ecnt_addr), "v"(1u) : "memory");
+                            if (pos < (uint32_t)(kWCap - 1)) {
+                                ekeys[pos] = score_key(v, row);
+                                eq[pos] = ql;
+                            } else {  // wave buffer full: straight to the global list
+                                const uint32_t q = qt * BN + ql;
+                                const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                                if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v, row);
+                                stored = true;
+                            }
+                        };
+                        // group maxima: group g = registers 4g..4g+3 = rows rbase + 8g + 0..3
+                        std::remove_reference_t<decltype(acc[m][n][0])> gm[4];
 #pragma unroll
-                        for (int r = 1; r < 16; ++r) mxv = mxv > acc[m][n][r] ? mxv : acc[m][n][r];
-                        if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
-                            // per-lane pass mask, then only the passing (lane, register)
-                            // pairs append
-                            uint32_t mask = 0;
+                        for (int g = 0; g < 4; ++g) {
+                            auto x = acc[m][n][4 * g], y = acc[m][n][4 * g + 2];
+                            x = x > acc[m][n][4 * g + 1] ? x : acc[m][n][4 * g + 1];
+                            y = y > acc[m][n][4 * g + 3] ? y : acc[m][n][4 * g + 3];
+                            gm[g] = x > y ? x : y;
+                        }
+                        auto mxv = gm[0] > gm[1] ? gm[0] : gm[1];
+                        mxv = mxv > gm[2] ? mxv : gm[2];
+                        mxv = mxv > gm[3] ? mxv : gm[3];
+                        if (EPI == 0) {
+                            // (the previous epilogue: per-lane mask over 16 registers)
+                            if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
+                                uint32_t mask = 0;
 #pragma unroll
-                            for (int r = 0; r < 16; ++r)
-                                mask |= (score(acc[m][n][r], sc[m], n) >= tau[n]) ? (1u << r) : 0u;
-                            while (mask) {
-                                const int r = __builtin_ctz(mask);
-                                mask &= mask - 1;
-                                const uint32_t row = rbase + (r & 3) + 8 * (r >> 2);
-                                if (row >= p.n_rows) continue;
-                                auto av = acc[m][n][0];
+                                for (int r = 0; r < 16; ++r)
+                                    mask |= (score(acc[m][n][r], sc[m], n) >= tau[n]) ? (1u << r) : 0u;
+                                while (mask) {
+                                    const int r = __builtin_ctz(mask);
+                                    mask &= mask - 1;
+                                    const uint32_t row = rbase + (r & 3) + 8 * (r >> 2);
+                                    if (row >= p.n_rows) continue;
+                                    auto av = acc[m][n][0];
 #pragma unroll
-                                for (int rr = 1; rr < 16; ++rr) av = (rr == r) ? acc[m][n][rr] : av;
-                                const float v = score(av, sc[m], n);
-                                uint32_t pos;
-                                asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-                                             : "=v"(pos) : "v"(ecnt_addr), "v"(1u) : "memory");
-                                if (pos < (uint32_t)(kWCap - 1)) {
-                                    ekeys[pos] = score_key(v, row);
-                                    eq[pos] = ql;
-                                } else {  // wave buffer full: straight to the global list
-                                    const uint32_t q = qt * BN + ql;
-                                    const uint32_t gp = atomicAdd(p.cnt + q, 1u);
-                                    if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v, row);
-                                    stored = true;
+                                    for (int rr = 1; rr < 16; ++rr) av = (rr == r) ? acc[m][n][rr] : av;
+                                    emit(score(av, sc[m], n), row);
+                                }
+                                stored = __ballot(stored) != 0;
+                            }
+                        } else if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
+                            // hierarchical: only groups whose maximum passes are expanded
+#pragma unroll
+                            for (int g = 0; g < 4; ++g) {
+                                if (!__ballot(score(gm[g], sc[m], n) >= tau[n])) continue;
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) {
+                                    const float v = score(acc[m][n][4 * g + i], sc[m], n);
+                                    const uint32_t row = rbase + 8 * g + i;
+                                    if (v >= tau[n] && row < p.n_rows) emit(v, row);
                                 }
                             }
                             stored = __ballot(stored) != 0;
                         }
                     }
+                    if (EPI == 0 || kNoMath) {  // (EPI >= 1: the next tile's first MFMAs take C = 0)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+                        for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+                    }
                 }
             }
             // global stores / atomics count in vmcnt: drain them so the counted waits stay exact
@@ -392,6 +452,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
             const uint32_t gp = atomicAdd(p.cnt + q, 1u);
             if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
         }
+    }
+    if (STAMP && tid == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x] = t1 - t0;
+        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x + 1] = r1 - r0;
     }
 }
 

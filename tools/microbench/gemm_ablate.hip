@@ -39,7 +39,9 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&A16, (size_t)npad * ld * 2)); CHECK(hipMalloc(&B16, (size_t)qpad * ld * 2));
     CHECK(hipMalloc(&A8, (size_t)npad * ld)); CHECK(hipMalloc(&B8, (size_t)qpad * ld));
     CHECK(hipMalloc(&as, npad / 32 * 4)); CHECK(hipMalloc(&bs, qpad * 4));
-    CHECK(hipMalloc(&tau, qpad * 4)); CHECK(hipMalloc(&cand, (size_t)qpad * cap * 8)); CHECK(hipMalloc(&cnt, qpad * 4));
+    CHECK(hipMalloc(&tau, qpad * 4));
+    uint64_t* stamp;
+    CHECK(hipMalloc(&stamp, 4096 * 16)); CHECK(hipMalloc(&cand, (size_t)qpad * cap * 8)); CHECK(hipMalloc(&cnt, qpad * 4));
     hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, (uint16_t*)A16, (size_t)npad * ld, 1);
     hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, (uint16_t*)B16, (size_t)qpad * ld, 2);
     hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
@@ -49,21 +51,25 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     GemmArgs g{};
     g.n_rows = n; g.a_row_mult = 1; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
+    g.S = reinterpret_cast<float*>(stamp);
     g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double flops = 2.0 * nq * (double)n * ld;
-    struct V { const char* name; void (*k)(GemmArgs); bool i8; float tau; std::vector<float> t; };
+    struct V { const char* name; void (*k)(GemmArgs); bool i8; float tau; std::vector<float> t; std::vector<double> clk; };
+    // every variant stamps its in-kernel clock (STAMP): the same instantiation is not the
+    // product build, whose kernels execute no stamp
     std::vector<V> vs = {
-        {"bf16 tau=inf", k_filter<OpBF16, true, 0>, false, 1e9f, {}},
-        {"bf16 tau=0.0415", k_filter<OpBF16, true, 0>, false, 0.0415f, {}},
-        {"bf16 no-DMA", k_filter<OpBF16, true, 1>, false, 1e9f, {}},
-        {"bf16 DMA-only", k_filter<OpBF16, true, 3>, false, 1e9f, {}},
-        {"i8 tau=inf", k_filter<OpI8, true, 0>, true, 1e9f, {}},
-        {"i8 noprio tau=inf", k_filter<OpI8, true, 0, false, false>, true, 1e9f, {}},
-        {"i8 noprio tau=0.125", k_filter<OpI8, true, 0, false, false>, true, 0.125f, {}},
-        {"i8 tau=0.125", k_filter<OpI8, true, 0>, true, 0.125f, {}},
-        {"i8 no-DMA", k_filter<OpI8, true, 1>, true, 1e9f, {}},
-        {"i8 DMA-only", k_filter<OpI8, true, 3>, true, 1e9f, {}},
+        {"bf16 tau=inf", k_filter<OpBF16, true, 0, false, false, 2, true>, false, 1e9f, {}, {}},
+        {"bf16 tau=0.0415", k_filter<OpBF16, true, 0, false, false, 2, true>, false, 0.0415f, {}, {}},
+        {"i8 tau=inf", k_filter<OpI8, true, 0, false, false, 2, true>, true, 1e9f, {}, {}},
+        {"i8 tau=0.125", k_filter<OpI8, true, 0, false, false, 2, true>, true, 0.125f, {}, {}},
+        {"i8 epi0 tau=0.125", k_filter<OpI8, true, 0, false, false, 0, true>, true, 0.125f, {}, {}},
+        {"i8 epi1 tau=0.125", k_filter<OpI8, true, 0, false, false, 1, true>, true, 0.125f, {}, {}},
+        {"i8 epi1 tau=inf", k_filter<OpI8, true, 0, false, false, 1, true>, true, 1e9f, {}, {}},
+        {"i8 no-epi", k_filter<OpI8, true, 5, false, false, 1, true>, true, 1e9f, {}, {}},
+        {"i8 no-DMA", k_filter<OpI8, true, 1, false, false, 1, true>, true, 1e9f, {}, {}},
+        {"i8 no-DMA no-epi", k_filter<OpI8, true, 6, false, false, 1, true>, true, 1e9f, {}, {}},
+        {"i8 DMA-only", k_filter<OpI8, true, 3, false, false, 1, true>, true, 1e9f, {}, {}},
     };
     if (only) {
         std::vector<V> keep;
@@ -85,7 +91,16 @@ int main(int argc, char** argv) {
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
             float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
-            if (r > 0) v.t.push_back(ms);
+            if (r > 0) {
+                v.t.push_back(ms);
+                std::vector<uint64_t> hs(2 * grid);
+                CHECK(hipMemcpy(hs.data(), stamp, hs.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<double> c;
+                for (uint32_t i = 0; i < grid; ++i)
+                    if (hs[2 * i + 1]) c.push_back((double)hs[2 * i] / hs[2 * i + 1] * 0.1);  // GHz (100 MHz ref)
+                std::sort(c.begin(), c.end());
+                if (!c.empty()) v.clk.push_back(c[c.size() / 2]);
+            }
             if (r == rounds - 1 && v.tau < 1e8f) {
                 std::vector<uint32_t> hc(qpad);
                 CHECK(hipMemcpy(hc.data(), cnt, qpad * 4, hipMemcpyDeviceToHost));
@@ -121,8 +136,11 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
         std::sort(v.t.begin(), v.t.end());
         float med = v.t[v.t.size() / 2], mn = v.t[0];
-        printf("%-18s median %7.3f ms  min %7.3f ms  (%7.1f T(FL)OP/s at median)\n", v.name, med, mn,
-               flops / (med * 1e-3) / 1e12);
+        std::sort(v.clk.begin(), v.clk.end());
+        const double clk = v.clk.empty() ? 0.0 : v.clk[v.clk.size() / 2];
+        printf("%-20s median %7.3f ms  min %7.3f ms  (%7.1f T(FL)OP/s at median)  clock %.2f GHz  (%4.0f%% of peak at that clock)\n",
+               v.name, med, mn, flops / (med * 1e-3) / 1e12, clk,
+               clk > 0 ? 100.0 * flops / (med * 1e-3) / (256.0 * 4 * (v.i8 ? 2048 : 1024) * clk * 1e9) : 0.0);
     }
     return 0;
 }
