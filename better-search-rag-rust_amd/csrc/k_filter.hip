@@ -461,6 +461,343 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------
+// Query-stationary int8 filter (the int8 default when a row is NK = 2..12 slices of 64
+// bytes, i.e. dims up to 768): one workgroup per CU, four waves (one per SIMD, ~420
+// VGPRs each).  Wave w keeps the int8 fragments of its 64 queries (qt*256 + 64w ..) for ALL
+// of K in registers for the workgroup's life, so only corpus rows stream through LDS:
+// 128-row tiles, one 64-byte K slice (8 KiB) per ring slot, 8 slots, 6 slices in flight,
+// one barrier per slice.  Per slice a wave reads 8 KiB of A fragments and issues 16 MFMAs
+// (128 rows x 64 queries x 64 bytes).  Per unit of work that is half the LDS-DMA bytes and
+// two thirds of the LDS-read bytes of k_filter (which re-stages its 256-query B tile for
+// every row tile and reads 192 B of fragments per k per 128x64 wave tile).
+// The K loop is unrolled per tile (the query registers need static indices), so the first
+// MFMAs of a tile take C = 0 without a branch.  Barrier wait: the slice read next has
+// landed for every wave (counted vmcnt: the DMAs of younger slices, and the tile's scale
+// load while it is younger, stay in flight) and this wave's fragment reads are complete.
+// Epilogue as k_filter (EMIT: group-maximum expansion; SAMPLE: scores or maxima to S).
+// ------------------------------------------------------------------------------------
+constexpr int kQsRows = 128;               // corpus rows per tile
+constexpr int kQsSlots = 8;                // LDS ring slots
+constexpr int kQsAhead = 6;                // slices issued ahead of the one being consumed
+constexpr int kQsSlot = kQsRows * kSliceB;  // 8 KiB
+constexpr int kQsWCap = 1024;              // candidate buffer entries per wave (one is the counter)
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier for a runtime N in [0, 15] (immediate operand).
+__device__ __forceinline__ void qs_barrier(uint32_t n) {
+#define BSR_QS_WAIT(N) \
+    case N: asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    switch (n) {
+        BSR_QS_WAIT(15) BSR_QS_WAIT(14) BSR_QS_WAIT(13) BSR_QS_WAIT(12) BSR_QS_WAIT(11) BSR_QS_WAIT(10)
+        BSR_QS_WAIT(9) BSR_QS_WAIT(8) BSR_QS_WAIT(7) BSR_QS_WAIT(6) BSR_QS_WAIT(5) BSR_QS_WAIT(4)
+        BSR_QS_WAIT(3) BSR_QS_WAIT(2) BSR_QS_WAIT(1)
+        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    }
+#undef BSR_QS_WAIT
+}
+
+template <int N>
+__device__ __forceinline__ void qs_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <bool EMIT, int NK, int NB, bool STAMP>
+__device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
+    // NB query blocks of 32 per wave: NB = 2 -> 4 waves x 64 queries (one wave per SIMD);
+    // NB = 1 -> 8 waves x 32 queries (two per SIMD, 96 query registers each)
+    constexpr int NW = 8 / NB, QW = 32 * NB, WCAP = NB == 2 ? kQsWCap : kQsWCap / 2;
+    uint64_t t0 = 0, r0 = 0, c_bar = 0, c_dma = 0, c_epi = 0;
+    if (STAMP) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+    // (STAMP: per-segment cycle counters of wave 0 -- barrier waits, DMA issue, epilogue)
+    auto stamp = [&]() -> uint64_t {
+        uint64_t t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    };
+    static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
+    constexpr int BM = kQsRows, BN = kFilterTile;
+    constexpr int EM_BYTES = EMIT ? NW * WCAP * 12 + NW * 64 * 64 : 0;  // + a 64-byte scratch row per lane
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[kQsSlots * kQsSlot + EM_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint64_t* ekeys = reinterpret_cast<uint64_t*>(lds + kQsSlots * kQsSlot) + w * WCAP;
+    uint32_t* eq = reinterpret_cast<uint32_t*>(lds + kQsSlots * kQsSlot + NW * WCAP * 8) + w * WCAP;
+    const uint32_t ecnt_addr = (uint32_t)(uintptr_t)(eq + WCAP - 1);
+    uint8_t* scr = lds + kQsSlots * kQsSlot + NW * WCAP * 12 + tid * 64;
+    if (EMIT && lane == 0) eq[WCAP - 1] = 0;
+
+    // Grid as k_filter: per XCD, G row groups x n_qt query tiles; a row tile's readers share
+    // the XCD's L2.
+    const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const uint32_t G = (gridDim.x >> 3) / p.n_qt;
+    const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
+    const bool active = slot < G * p.n_qt;
+    const uint32_t qt = active ? slot % p.n_qt : 0;
+    const uint32_t g0 = xcd * G + (active ? slot / p.n_qt : 0);
+    const uint32_t RG = 8 * G;
+    const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
+    const uint32_t J = my_rt * NK;
+
+    // The wave's query fragments, all K: fb[n][s] = queries .. + n*32 + (lane & 31),
+    // bytes 32s + 16(lane >> 5) .. +15 (the MFMA B layout).
+    i32x4_t fb[NB][2 * NK];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+        const uint8_t* src = p.B + (uint64_t)(qt * BN + w * QW + n * 32 + (lane & 31)) * p.row_bytes + 16 * (lane >> 5);
+#pragma unroll
+        for (int s2 = 0; s2 < 2 * NK; ++s2) fb[n][s2] = *reinterpret_cast<const i32x4_t*>(src + 32 * s2);
+    }
+    float tau[NB], sbq[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+        const uint32_t q = qt * BN + w * QW + n * 32 + (lane & 31);
+        tau[n] = 0.0f;
+        if (EMIT) tau[n] = p.tau[q];
+        sbq[n] = p.b_scale[q];
+    }
+
+    // LDS-DMA: wave w fills rows (2w+i)*16 .. +15 of each slice (1 KiB per instruction),
+    // XOR-swizzled on the source chunk as k_filter.
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t lrow[NB], aoff_dma[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        lrow[i] = (w * NB + i) * 16 + (lane >> 2);
+        aoff_dma[i] = lrow[i] * (uint32_t)p.a_stride + (((lane & 3) ^ ((lrow[i] >> 2) & 3)) * 16);
+    }
+    uint32_t iss_ti = 0, iss_kt = 0;
+    __amdgpu_buffer_rsrc_t rsrc_a;
+    auto set_issue_tile = [&]() {
+        const uint32_t rt = g0 + iss_ti * RG;
+        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
+                                                   BM * (uint32_t)p.a_stride, 0x00020000);
+        if (!EMIT) {  // sample pass: tail rows read the last valid row
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const uint32_t r = rt * BM + lrow[i] < p.n_rows ? lrow[i] : p.n_rows - 1 - rt * BM;
+                aoff_dma[i] = r * (uint32_t)p.a_stride + (((lane & 3) ^ ((lrow[i] >> 2) & 3)) * 16);
+            }
+        }
+    };
+    // DMA i (< NB) of slice jj = (iss_ti, iss_kt); the last advances the issue state
+    auto issue_dma = [&](uint32_t jj, int i) {
+        uint8_t* la = lds + (jj % kQsSlots) * kQsSlot + wu * (NB * 1024) + i * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma[i], iss_kt * kSliceB, 0, 0);
+        if (i == NB - 1 && ++iss_kt == NK) {
+            iss_kt = 0;
+            ++iss_ti;
+            if (iss_ti < my_rt) set_issue_tile();
+        }
+    };
+
+    int aoff[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int row = m * 32 + (lane & 31);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int lc = 2 * kk + (lane >> 5);
+            aoff[m][kk] = row * kSliceB + ((lc ^ ((row >> 2) & 3)) * 16);
+        }
+    }
+    // A fragments [m][kk]; fa[.][kk] of the next slice are read as soon as this slice's kk
+    // MFMAs have issued (one register set: the query fragments fill most of the file)
+    i32x4_t fa[4][2];
+    auto read_frag = [&](uint32_t jj, int m, int kk) {
+        fa[m][kk] = *reinterpret_cast<const i32x4_t*>(lds + (jj % kQsSlots) * kQsSlot + aoff[m][kk]);
+    };
+
+    i32x16_t acc[4][NB];
+    // Prologue: slices 0..min(J, kQsAhead)-1 issued; slice 0 landed everywhere; its
+    // fragments read.
+    if (my_rt) set_issue_tile();
+    const uint32_t pre = J < (uint32_t)kQsAhead ? J : (uint32_t)kQsAhead;
+    for (uint32_t jj = 0; jj < pre; ++jj)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) issue_dma(jj, i);
+    qs_barrier(pre >= 2 ? NB * (pre - 2) : 0);  // slices 0 and 1 landed everywhere
+    if (J)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) { read_frag(0, m, 0); read_frag(0, m, 1); }
+
+    for (uint32_t t = 0; t < my_rt; ++t) {
+        const uint32_t rt = g0 + t * RG;
+        float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) {
+            const uint32_t jj = t * NK + kt;
+            // Per K half, per m: the two MFMAs of A block m, then the next slice's fragment
+            // of block m (landed: previous barrier; the register is free once both MFMAs
+            // issued).  The DMAs of slice jj + kQsAhead and the barrier sit between MFMA
+            // pairs, so one wave per SIMD keeps its MFMA pipe fed while they issue.
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+#pragma unroll
+                    for (int n = 0; n < NB; ++n) {
+                        if (kt == 0 && kk == 0) {
+                            const i32x16_t z = {};
+                            acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m][kk], fb[n][2 * kt + kk], z, 0, 0, 0);
+                        } else {
+                            acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m][kk], fb[n][2 * kt + kk], acc[m][n], 0, 0, 0);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    read_frag(jj + 1, m, kk);  // (past the stream's end: unused; unconditional
+                                               // so hipcc can count the LDS reads exactly)
+                    if (kk == 0 && (m & 1) && (m >> 1) < NB && jj + kQsAhead < J) {
+                        uint64_t ts = 0;
+                        if (STAMP) ts = stamp();
+                        issue_dma(jj + kQsAhead, m >> 1);
+                        if (STAMP) c_dma += stamp() - ts;
+                    }
+                    uint64_t tb = 0;
+                    if (STAMP && kk == 1 && m == 1) tb = stamp();
+                    if (kk == 1 && m == 1) {
+                        // the slice after next has landed everywhere: younger DMAs (2 per
+                        // slice) and the scale load (issued at kt = 0, younger than slices
+                        // up to jj + 4) stay in flight.  No lgkmcnt: the slot a DMA refills
+                        // next step was read two steps ago (waited before its MFMAs).
+                        if (jj + kQsAhead < J) {
+                            if (EMIT && kt <= 3) qs_wait<NB * (kQsAhead - 2) + 1>();  // (kt folds: unrolled)
+                            else qs_wait<NB * (kQsAhead - 2)>();
+                        } else if (jj + 1 < J) {  // the stream's last slices: counted at run time
+                            const uint32_t younger = J - 1 > jj + 2 ? NB * (J - 1 - jj - 2) : 0;
+                            qs_barrier(younger + ((EMIT && kt <= 3) ? 1 : 0));
+                        }
+                    }
+                    if (STAMP && kk == 1 && m == 1) c_bar += stamp() - tb;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        // ---- epilogue
+        uint64_t te = 0;
+        if (STAMP) te = stamp();
+        bool stored = false;
+        const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+#pragma unroll
+            for (int n = 0; n < NB; ++n) {
+                const uint32_t ql = w * QW + n * 32 + (lane & 31);
+                const uint32_t rbase = rt * BM + m * 32 + 4 * (lane >> 5);
+                auto score = [&](int v, float s_r) -> float { return ((float)v * s_r) * sbq[n]; };
+                if constexpr (!EMIT) {
+                    float v[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
+                        tr = tr < p.n_rows ? tr : p.n_rows - 1;
+                        v[r] = score(acc[m][n][r], p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]);
+                    }
+                    float* srow = p.S + (uint64_t)(qt * BN + ql) * p.s_ld;
+                    if (!p.s_compact) {
+#pragma unroll
+                        for (int g = 0; g < 4; ++g)
+                            *reinterpret_cast<float4*>(srow + rbase + 8 * g) =
+                                make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+                    } else {
+                        float mx = v[0];
+#pragma unroll
+                        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, v[r]);
+                        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                        if (lane < 32) srow[(rt * BM + m * 32) / 32] = mx;
+                    }
+                    stored = true;
+                } else {
+                    auto emit = [&](float v, uint32_t row) {
+                        uint32_t pos;
+                        asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                                     : "=v"(pos) : "v"(ecnt_addr), "v"(1u) : "memory");
+                        // (a full buffer keeps counting: the flush marks the wave's queries)
+                        if (pos < (uint32_t)(WCAP - 1)) {
+                            ekeys[pos] = score_key(v, row);
+                            eq[pos] = ql;
+                        }
+                    };
+                    int gm[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int x = max(acc[m][n][4 * g], acc[m][n][4 * g + 1]);
+                        const int y = max(acc[m][n][4 * g + 2], acc[m][n][4 * g + 3]);
+                        gm[g] = max(x, y);
+                    }
+                    const int mxv = max(max(gm[0], gm[1]), max(gm[2], gm[3]));
+                    if (__ballot(score(mxv, sc[m]) >= tau[n])) {
+                        // passing registers of the groups whose maximum passes, then one
+                        // append site per block (register picked by a select chain)
+                        uint32_t mask = 0;
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) {
+                            if (!__ballot(score(gm[g], sc[m]) >= tau[n])) continue;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                mask |= (score(acc[m][n][4 * g + i], sc[m]) >= tau[n] && rbase + 8 * g + i < p.n_rows)
+                                            ? 1u << (4 * g + i) : 0u;
+                        }
+                        // the lane's 16 values go through its LDS scratch row, so the
+                        // register r is picked by address (a select chain over the
+                        // accumulators would hold them all in VGPRs at once)
+                        if (mask) {
+#pragma unroll
+                            for (int g = 0; g < 4; ++g)
+                                *reinterpret_cast<i32x4_t*>(scr + 16 * g) =
+                                    i32x4_t{acc[m][n][4 * g], acc[m][n][4 * g + 1], acc[m][n][4 * g + 2], acc[m][n][4 * g + 3]};
+                        }
+                        while (mask) {
+                            const int r = __builtin_ctz(mask);
+                            mask &= mask - 1;
+                            const int av = reinterpret_cast<const int*>(scr)[r];
+                            emit(score(av, sc[m]), rbase + 8 * (r >> 2) + (r & 3));
+                        }
+                    }
+                }
+            }
+        }
+        // global stores / atomics count in vmcnt: drain them so the counted waits stay exact
+        if (stored) wait_vm0();
+        if (STAMP) c_epi += stamp() - te;
+    }
+    if constexpr (EMIT) {
+        const uint32_t ecount = eq[WCAP - 1];
+        const uint32_t ne = ecount < (uint32_t)(WCAP - 1) ? ecount : (uint32_t)(WCAP - 1);
+        for (uint32_t i = lane; i < ne; i += kWave) {
+            const uint32_t q = qt * BN + eq[i];
+            const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+            if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
+        }
+        // candidates were dropped (never at a sane tau): every query of the wave is marked
+        // overflowed (count > cap), so none of them is certified from this list
+        if (ecount > (uint32_t)(WCAP - 1) && lane < QW) atomicAdd(p.cnt + qt * BN + w * QW + lane, p.cap + 1u);
+    }
+    if (STAMP && tid == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x] = t1 - t0;
+        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x + 1] = r1 - r0;
+        uint64_t* seg = reinterpret_cast<uint64_t*>(p.S) + 2 * gridDim.x + 4 * blockIdx.x;
+        seg[0] = c_bar;
+        seg[1] = c_dma;
+        seg[2] = c_epi;
+        seg[3] = J;
+    }
+}
+
+// One wave per SIMD (NB = 2) and two per SIMD (NB = 1): separate kernels, so each gets
+// its register budget from a plain __launch_bounds__.
+template <bool EMIT, int NK, int NB = 2, bool STAMP = false>
+__global__ __launch_bounds__(256, 1) void k_filter_qs(GemmArgs p) {
+    static_assert(NB == 2, "k_filter_qs: 4 waves x 64 queries");
+    filter_qs_body<EMIT, NK, 2, STAMP>(p);
+}
+template <bool EMIT, int NK, bool STAMP = false>
+__global__ __launch_bounds__(512, 1) void k_filter_qs8(GemmArgs p) {
+    filter_qs_body<EMIT, NK, 1, STAMP>(p);
+}
+
+// ------------------------------------------------------------------------------------
 // Skinny int8 filter for batches of at most 16 queries (single-query latency path): the
 // work is HBM-bound (1 byte per element), so there is no LDS staging.  Each wave walks
 // groups of 32 tile rows; per 64-byte K step a lane loads its 16-byte A fragments straight
@@ -782,18 +1119,32 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s) {
+// int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
+// query-stationary kernel; other int8 widths and bf16: k_filter.
+template <bool EMIT>
+static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s) {
+    const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
+    if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
+        switch (nk) {
+            case 2: hipLaunchKernelGGL((k_filter_qs8<EMIT, 2, false>), dim3(grid), dim3(512), 0, s, a); return;
+            case 4: hipLaunchKernelGGL((k_filter_qs8<EMIT, 4, false>), dim3(grid), dim3(512), 0, s, a); return;
+            case 6: hipLaunchKernelGGL((k_filter_qs8<EMIT, 6, false>), dim3(grid), dim3(512), 0, s, a); return;
+            case 8: hipLaunchKernelGGL((k_filter_qs8<EMIT, 8, false>), dim3(grid), dim3(512), 0, s, a); return;
+            case 10: hipLaunchKernelGGL((k_filter_qs8<EMIT, 10, false>), dim3(grid), dim3(512), 0, s, a); return;
+            default: hipLaunchKernelGGL((k_filter_qs8<EMIT, 12, false>), dim3(grid), dim3(512), 0, s, a); return;
+        }
+    }
     if (op == kFilterI8)
-        hipLaunchKernelGGL((k_filter<OpI8, false>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), 0, s, a);
     else
-        hipLaunchKernelGGL((k_filter<OpBF16, false>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_filter<OpBF16, EMIT>), dim3(grid), dim3(kThreads), 0, s, a);
+}
+hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s) {
+    launch_filter<false>(op, a, s);
     return hipGetLastError();
 }
 hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s) {
-    if (op == kFilterI8)
-        hipLaunchKernelGGL((k_filter<OpI8, true>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_filter<OpBF16, true>), dim3(filter_grid(a.n_qt)), dim3(kThreads), 0, s, a);
+    launch_filter<true>(op, a, s);
     return hipGetLastError();
 }
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,

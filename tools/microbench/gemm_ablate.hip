@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
     g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double flops = 2.0 * nq * (double)n * ld;
-    struct V { const char* name; void (*k)(GemmArgs); bool i8; float tau; std::vector<float> t; std::vector<double> clk; };
+    struct V { const char* name; void (*k)(GemmArgs); bool i8; float tau; std::vector<float> t; std::vector<double> clk; int threads = 512; };
     // every variant stamps its in-kernel clock (STAMP): the same instantiation is not the
     // product build, whose kernels execute no stamp
     std::vector<V> vs = {
@@ -70,6 +70,13 @@ int main(int argc, char** argv) {
         {"i8 no-DMA", k_filter<OpI8, true, 1, false, false, 1, true>, true, 1e9f, {}, {}},
         {"i8 no-DMA no-epi", k_filter<OpI8, true, 6, false, false, 1, true>, true, 1e9f, {}, {}},
         {"i8 DMA-only", k_filter<OpI8, true, 3, false, false, 1, true>, true, 1e9f, {}, {}},
+        {"qs tau=inf", k_filter_qs<true, 12, 2, true>, true, 1e9f, {}, {}, 256},
+        {"qs tau=0.125", k_filter_qs<true, 12, 2, true>, true, 0.125f, {}, {}, 256},
+        {"qs2 tau=inf", k_filter_qs8<true, 12, true>, true, 1e9f, {}, {}, 512},
+        {"qs2 tau=0.125", k_filter_qs8<true, 12, true>, true, 0.125f, {}, {}, 512},
+        {"Qs2 nostamp tau=inf", k_filter_qs8<true, 12, false>, true, 1e9f, {}, {}, 512},
+        {"Qs2 nostamp tau=0.125", k_filter_qs8<true, 12, false>, true, 0.125f, {}, {}, 512},
+        {"Qs nostamp tau=0.125", k_filter_qs<true, 12, 2, false>, true, 0.125f, {}, {}, 256},
     };
     if (only) {
         std::vector<V> keep;
@@ -86,8 +93,9 @@ int main(int argc, char** argv) {
             std::vector<float> ht(qpad, v.tau);
             CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
             CHECK(hipMemset(cnt, 0, qpad * 4));
+            CHECK(hipMemset(stamp, 0, 4096 * 16));
             CHECK(hipEventRecord(e0));
-            hipLaunchKernelGGL(v.k, dim3(grid), dim3(512), 0, 0, g);
+            hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, g);
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
             float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -100,6 +108,16 @@ int main(int argc, char** argv) {
                     if (hs[2 * i + 1]) c.push_back((double)hs[2 * i] / hs[2 * i + 1] * 0.1);  // GHz (100 MHz ref)
                 std::sort(c.begin(), c.end());
                 if (!c.empty()) v.clk.push_back(c[c.size() / 2]);
+                if (r == rounds - 1 && strncmp(v.name, "qs", 2) == 0) {  // qs: per-segment cycles of wave 0
+                    std::vector<uint64_t> sg(4 * grid);
+                    CHECK(hipMemcpy(sg.data(), stamp + 2 * grid, sg.size() * 8, hipMemcpyDeviceToHost));
+                    double tb = 0, td = 0, te = 0, tj = 0, tt = 0;
+                    for (uint32_t i = 0; i < grid; ++i) {
+                        tb += sg[4 * i]; td += sg[4 * i + 1]; te += sg[4 * i + 2]; tj += sg[4 * i + 3]; tt += hs[2 * i];
+                    }
+                    printf("  [%s] per slice: total %.0f cyc, barrier %.0f, dma issue %.0f, epilogue %.0f (slices/WG %.0f)\n",
+                           v.name, tt / tj, tb / tj, td / tj, te / tj, tj / grid);
+                }
             }
             if (r == rounds - 1 && v.tau < 1e8f) {
                 std::vector<uint32_t> hc(qpad);
