@@ -4,7 +4,7 @@ Workload (BASELINE.json configs[1] per GPU): every rank holds a 1M-row shard of 
 768-d U(-1,1) f32 corpus (the shard is interval_by_rank(rank, N, N*1M) of one global corpus
 generated on the device), 1000 queries (query 0 = corpus row 0, the reference's self-query),
 top-10.  One step = parallel_top_k_similarity_search for the whole query batch: local search
-on every GPU (bf16 MFMA filter + exact f32 rescore), RCCL all-gather of the partial lists,
+on every GPU (int8 MFMA candidate filter + exact f32 rescore), RCCL all-gather of the partial lists,
 host merge on rank 0.  Weak scaling: the corpus grows with N (1M rows per GPU); `value`
 counts each query once per 1M-row shard, so at N=1 it is plain queries/s over 1M vectors.
 
@@ -166,7 +166,11 @@ def main():
         achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
         traffic = None
         peak = PEAK_I8_DENSE if args.filter == "i8" else PEAK_BF16_DENSE
-        kname = f"k_filter<Op{'I8' if args.filter == 'i8' else 'BF16'}, true>"
+        nk = (D + 63) // 64
+        if args.filter == "i8":
+            kname = f"k_filter_qs8<true, {nk}>" if nk % 2 == 0 and nk <= 12 else "k_filter<OpI8, true>"
+        else:
+            kname = "k_filter<OpBF16, true>"
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
@@ -199,7 +203,7 @@ def main():
                 "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank) + RCCL all-gather",
                 "filter": ("int8 MFMA (v_mfma_i32_32x32x32_i8) candidates" if args.filter == "i8" else
                            "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates") +
-                          ", exact sequential-f32 rescore of k'=63 per query, certified (DESIGN.md §4)",
+                          f", exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)",
                 "qps_over_full_corpus": round(Q / (ms_per_step * 1e-3), 2),
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
@@ -239,7 +243,9 @@ def main():
         # (N*ld*4 bytes).
         if args.filter == "i8":
             kms = prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1)
-            kbytes, kn = n_local * ((D + 63) // 64 * 64), "k_filter_skinny<true>"
+            nk = (D + 63) // 64
+            kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
+            kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>")
         else:
             kms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)
             kbytes, kn = n_local * ((D + 63) // 64 * 64) * 4, "k_scan_exact<1,1>"

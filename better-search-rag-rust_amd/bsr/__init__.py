@@ -29,7 +29,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr.so")
+# (BSR_LIB: another build of the same ABI, for A/B measurements)
+LIB_PATH = os.environ.get("BSR_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libbsr.so")
 VSTORE_LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr_vstore.so")
 
 BSR_OK = 0

@@ -480,7 +480,7 @@ constexpr int kQsRows = 128;               // corpus rows per tile
 constexpr int kQsSlots = 8;                // LDS ring slots
 constexpr int kQsAhead = 6;                // slices issued ahead of the one being consumed
 constexpr int kQsSlot = kQsRows * kSliceB;  // 8 KiB
-constexpr int kQsWCap = 1024;              // candidate buffer entries per wave (one is the counter)
+constexpr int kQsLaneCap = 20;             // candidate ring entries per (lane, query block)
 
 // s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier for a runtime N in [0, 15] (immediate operand).
 __device__ __forceinline__ void qs_barrier(uint32_t n) {
@@ -499,12 +499,27 @@ template <int N>
 __device__ __forceinline__ void qs_wait() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// qs_wait<n> for an n that folds to a constant once the K loop is unrolled
+__device__ __forceinline__ void qs_wait_n(int n) {
+#define BSR_QS_N(N) \
+    case N: qs_wait<N>(); break;
+    switch (n) {
+        BSR_QS_N(1) BSR_QS_N(2) BSR_QS_N(3) BSR_QS_N(4) BSR_QS_N(5) BSR_QS_N(6) BSR_QS_N(7) BSR_QS_N(8)
+        BSR_QS_N(9) BSR_QS_N(10) BSR_QS_N(11) BSR_QS_N(12) BSR_QS_N(13) BSR_QS_N(14) BSR_QS_N(15)
+        default: qs_wait<0>(); break;
+    }
+#undef BSR_QS_N
+}
 
-template <bool EMIT, int NK, int NB, bool STAMP>
+// VAR (tooling): 1 = no LDS-DMA in the loop, 5 = no epilogue, 6 = neither.  STAG (tooling):
+// waves 4-7 take each slice's barrier half a slice earlier than their SIMD partners (waves
+// 0-3).
+template <bool EMIT, int NK, int NB, bool STAMP, int VAR = 0, bool STAG = false>
 __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
+    constexpr bool kNoDMA = VAR == 1 || VAR == 6, kNoEpi = VAR == 5 || VAR == 6;
     // NB query blocks of 32 per wave: NB = 2 -> 4 waves x 64 queries (one wave per SIMD);
     // NB = 1 -> 8 waves x 32 queries (two per SIMD, 96 query registers each)
-    constexpr int NW = 8 / NB, QW = 32 * NB, WCAP = NB == 2 ? kQsWCap : kQsWCap / 2;
+    constexpr int NT = 64 * (8 / NB), QW = 32 * NB;
     uint64_t t0 = 0, r0 = 0, c_bar = 0, c_dma = 0, c_epi = 0;
     if (STAMP) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
     // (STAMP: per-segment cycle counters of wave 0 -- barrier waits, DMA issue, epilogue)
@@ -517,14 +532,18 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     };
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
     constexpr int BM = kQsRows, BN = kFilterTile;
-    constexpr int EM_BYTES = EMIT ? NW * WCAP * 12 + NW * 64 * 64 : 0;  // + a 64-byte scratch row per lane
+    // LDS: the ring; then (EMIT) a private candidate ring of kQsLaneCap keys per (lane, query
+    // block), entry e of thread t at [e][t] (conflict-free), its count in a register: no
+    // atomics and no waits in the epilogue, the rings go to the per-query global lists once,
+    // at the end (earlier if a block's rows could overfill it).
+    constexpr int EM_BYTES = EMIT ? NT * NB * kQsLaneCap * 8 : 0;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[kQsSlots * kQsSlot + EM_BYTES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint64_t* ekeys = reinterpret_cast<uint64_t*>(lds + kQsSlots * kQsSlot) + w * WCAP;
-    uint32_t* eq = reinterpret_cast<uint32_t*>(lds + kQsSlots * kQsSlot + NW * WCAP * 8) + w * WCAP;
-    const uint32_t ecnt_addr = (uint32_t)(uintptr_t)(eq + WCAP - 1);
-    uint8_t* scr = lds + kQsSlots * kQsSlot + NW * WCAP * 12 + tid * 64;
-    if (EMIT && lane == 0) eq[WCAP - 1] = 0;
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds + kQsSlots * kQsSlot) + tid;
+    uint32_t ecnt[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) ecnt[n] = 0;
 
     // Grid as k_filter: per XCD, G row groups x n_qt query tiles; a row tile's readers share
     // the XCD's L2.
@@ -555,10 +574,20 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
         if (EMIT) tau[n] = p.tau[q];
         sbq[n] = p.b_scale[q];
     }
+    // the lane's ring of query block n to the query's global list (a count past cap marks the
+    // list overflowed: not certified from it)
+    auto flush_ring = [&](int n) {
+        const uint32_t q = qt * BN + w * QW + n * 32 + (lane & 31), nn = ecnt[n];
+        if (nn) {
+            const uint32_t gp = atomicAdd(p.cnt + q, nn);
+            for (uint32_t i = 0; i < nn; ++i)
+                if (gp + i < p.cap) p.cand[(uint64_t)q * p.cap + gp + i] = lkeys[(n * kQsLaneCap + i) * NT];
+        }
+        ecnt[n] = 0;
+    };
 
-    // LDS-DMA: wave w fills rows (2w+i)*16 .. +15 of each slice (1 KiB per instruction),
+    // LDS-DMA: wave w fills rows (NB*w+i)*16 .. +15 of each slice (1 KiB per instruction),
     // XOR-swizzled on the source chunk as k_filter.
-    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t lrow[NB], aoff_dma[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -622,6 +651,8 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
 
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
+        // the tile's block scales: a plain load (hipcc drains vmcnt(0) at its use in the
+        // epilogue; an LDS-DMA of the scales, which avoids that drain, measured 5% slower)
         float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
 #pragma unroll
@@ -647,31 +678,37 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     __builtin_amdgcn_sched_barrier(0);
                     read_frag(jj + 1, m, kk);  // (past the stream's end: unused; unconditional
                                                // so hipcc can count the LDS reads exactly)
-                    if (kk == 0 && (m & 1) && (m >> 1) < NB && jj + kQsAhead < J) {
+                    if (!kNoDMA && kk == 0 && (m & 1) && (m >> 1) < NB && jj + kQsAhead < J) {
                         uint64_t ts = 0;
                         if (STAMP) ts = stamp();
                         issue_dma(jj + kQsAhead, m >> 1);
                         if (STAMP) c_dma += stamp() - ts;
                     }
-                    uint64_t tb = 0;
-                    if (STAMP && kk == 1 && m == 1) tb = stamp();
-                    if (kk == 1 && m == 1) {
-                        // the slice after next has landed everywhere: younger DMAs (2 per
-                        // slice) and the scale load (issued at kt = 0, younger than slices
-                        // up to jj + 4) stay in flight.  No lgkmcnt: the slot a DMA refills
-                        // next step was read two steps ago (waited before its MFMAs).
+                    // Barrier: the slice after next has landed everywhere.  Younger VMEM ops
+                    // stay in flight: the DMAs of slices jj+3 .. jj+kQsAhead (NB each) and,
+                    // while it is younger than slice jj+2 (kt <= 3), the tile's scale load.
+                    // No lgkmcnt: the slot a DMA refills next step was read two steps ago
+                    // (hipcc waited for those reads before their MFMAs).
+                    if (m == 1 && kk == ((STAG && wu >= 4) ? 0 : 1)) {
+                        uint64_t tb = 0;
+                        if (STAMP) tb = stamp();
                         if (jj + kQsAhead < J) {
-                            if (EMIT && kt <= 3) qs_wait<NB * (kQsAhead - 2) + 1>();  // (kt folds: unrolled)
-                            else qs_wait<NB * (kQsAhead - 2)>();
-                        } else if (jj + 1 < J) {  // the stream's last slices: counted at run time
-                            const uint32_t younger = J - 1 > jj + 2 ? NB * (J - 1 - jj - 2) : 0;
-                            qs_barrier(younger + ((EMIT && kt <= 3) ? 1 : 0));
+                            qs_wait_n(NB * (kQsAhead - 2) + ((EMIT && kt <= 3) ? 1 : 0));  // (folds: kt unrolled)
+                        } else if (jj + 1 < J) {  // the stream's last slices, counted at run time
+                            qs_barrier((J - 1 > jj + 2 ? NB * (J - 1 - jj - 2) : 0) + ((EMIT && kt <= 3) ? 1 : 0));
                         }
+                        if (STAMP) c_bar += stamp() - tb;
                     }
-                    if (STAMP && kk == 1 && m == 1) c_bar += stamp() - tb;
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+        }
+        if constexpr (kNoEpi) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < NB; ++n) asm volatile("" ::"v"(acc[m][n][0]));
+            continue;
         }
         // ---- epilogue
         uint64_t te = 0;
@@ -709,14 +746,8 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     stored = true;
                 } else {
                     auto emit = [&](float v, uint32_t row) {
-                        uint32_t pos;
-                        asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-                                     : "=v"(pos) : "v"(ecnt_addr), "v"(1u) : "memory");
-                        // (a full buffer keeps counting: the flush marks the wave's queries)
-                        if (pos < (uint32_t)(WCAP - 1)) {
-                            ekeys[pos] = score_key(v, row);
-                            eq[pos] = ql;
-                        }
+                        lkeys[(n * kQsLaneCap + ecnt[n]) * NT] = score_key(v, row);
+                        ++ecnt[n];
                     };
                     int gm[4];
 #pragma unroll
@@ -727,31 +758,20 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     }
                     const int mxv = max(max(gm[0], gm[1]), max(gm[2], gm[3]));
                     if (__ballot(score(mxv, sc[m]) >= tau[n])) {
-                        // passing registers of the groups whose maximum passes, then one
-                        // append site per block (register picked by a select chain)
-                        uint32_t mask = 0;
+                        // room for this block's up to 16 rows in every lane's ring (rarely
+                        // not: dense emission, e.g. large k)
+                        if (__ballot(ecnt[n] > (uint32_t)(kQsLaneCap - 16))) flush_ring(n);
+                        // only the groups whose maximum passes are expanded; each register
+                        // appends under its own lane mask
 #pragma unroll
                         for (int g = 0; g < 4; ++g) {
                             if (!__ballot(score(gm[g], sc[m]) >= tau[n])) continue;
 #pragma unroll
-                            for (int i = 0; i < 4; ++i)
-                                mask |= (score(acc[m][n][4 * g + i], sc[m]) >= tau[n] && rbase + 8 * g + i < p.n_rows)
-                                            ? 1u << (4 * g + i) : 0u;
-                        }
-                        // the lane's 16 values go through its LDS scratch row, so the
-                        // register r is picked by address (a select chain over the
-                        // accumulators would hold them all in VGPRs at once)
-                        if (mask) {
-#pragma unroll
-                            for (int g = 0; g < 4; ++g)
-                                *reinterpret_cast<i32x4_t*>(scr + 16 * g) =
-                                    i32x4_t{acc[m][n][4 * g], acc[m][n][4 * g + 1], acc[m][n][4 * g + 2], acc[m][n][4 * g + 3]};
-                        }
-                        while (mask) {
-                            const int r = __builtin_ctz(mask);
-                            mask &= mask - 1;
-                            const int av = reinterpret_cast<const int*>(scr)[r];
-                            emit(score(av, sc[m]), rbase + 8 * (r >> 2) + (r & 3));
+                            for (int i = 0; i < 4; ++i) {
+                                const float v = score(acc[m][n][4 * g + i], sc[m]);
+                                const uint32_t row = rbase + 8 * g + i;
+                                if (v >= tau[n] && row < p.n_rows) emit(v, row);
+                            }
                         }
                     }
                 }
@@ -762,16 +782,8 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
         if (STAMP) c_epi += stamp() - te;
     }
     if constexpr (EMIT) {
-        const uint32_t ecount = eq[WCAP - 1];
-        const uint32_t ne = ecount < (uint32_t)(WCAP - 1) ? ecount : (uint32_t)(WCAP - 1);
-        for (uint32_t i = lane; i < ne; i += kWave) {
-            const uint32_t q = qt * BN + eq[i];
-            const uint32_t gp = atomicAdd(p.cnt + q, 1u);
-            if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
-        }
-        // candidates were dropped (never at a sane tau): every query of the wave is marked
-        // overflowed (count > cap), so none of them is certified from this list
-        if (ecount > (uint32_t)(WCAP - 1) && lane < QW) atomicAdd(p.cnt + qt * BN + w * QW + lane, p.cap + 1u);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) flush_ring(n);
     }
     if (STAMP && tid == 0) {
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -792,9 +804,9 @@ __global__ __launch_bounds__(256, 1) void k_filter_qs(GemmArgs p) {
     static_assert(NB == 2, "k_filter_qs: 4 waves x 64 queries");
     filter_qs_body<EMIT, NK, 2, STAMP>(p);
 }
-template <bool EMIT, int NK, bool STAMP = false>
+template <bool EMIT, int NK, bool STAMP = false, int VAR = 0, bool STAG = false>
 __global__ __launch_bounds__(512, 1) void k_filter_qs8(GemmArgs p) {
-    filter_qs_body<EMIT, NK, 1, STAMP>(p);
+    filter_qs_body<EMIT, NK, 1, STAMP, VAR, STAG>(p);
 }
 
 // ------------------------------------------------------------------------------------

@@ -166,6 +166,37 @@ def test_large_k_certifies_without_fallback(bsr_mod, oracle_mod, gpu):
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 100), "k=100")
 
 
+def test_large_k_many_queries_dense_emission(bsr_mod, oracle_mod, gpu):
+    # 2048 queries, k = 100: every filter workgroup sees ~48 emitted rows per query, more
+    # than a lane's candidate ring holds (the rest append to the global lists directly).
+    # All queries must still certify; parity on a subset (the oracle's cost).
+    rng = np.random.default_rng(33)
+    rows = rng.uniform(-1, 1, (100000, 768)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (2048, 768)).astype(np.float32)
+    qs[0] = rows[777]
+    ix = _index(bsr_mod, rows, max_k=100)
+    gi, gd, gc = ix.local_top_k(qs, 100)
+    st = ix.last_stats()
+    assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
+    sub = np.r_[0:8, 1020:1024, 2040:2048]
+    _assert_same((gi[sub], gd[sub], gc[sub]), oracle_mod.parallel_top_k(rows, qs[sub], 100), "k=100 Q=2048")
+
+
+@FILTERS
+def test_duplicate_runs_overflow_lane_rings(bsr_mod, oracle_mod, gpu, fflags):
+    # Runs of 400 identical rows: a query equal to one of them passes the filter on a whole
+    # run (64 rows per lane per tile, more than a lane's candidate ring); ties resolve by
+    # index and every result stays exact (through the fallback when uncertifiable).
+    rng = np.random.default_rng(5)
+    base = rng.uniform(-1, 1, (100, 768)).astype(np.float32)
+    rows = np.repeat(base, 400, axis=0)
+    qs = base[rng.integers(0, 100, 40)].copy()
+    qs[1::2] += rng.uniform(-0.05, 0.05, (20, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, flags=fflags)
+    got = ix.local_top_k(qs, 10)
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "duplicate runs")
+
+
 @FILTERS
 def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu, fflags):
     # Clustered embeddings (dense neighbourhoods) stress the certification; any query it

@@ -11,16 +11,18 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 
-timeout -k 10 120 ./tools/microbench/gemm_ablate 1000000 1000 6 > "$O/gemm_ablate.txt" 2>&1
+timeout -k 10 180 ./tools/microbench/gemm_ablate 1000000 1000 10 > "$O/gemm_ablate.txt" 2>&1
 rc=$?; echo "microbench rc=$rc"; ok $rc || exit $rc
 
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 "$O/pytest_gpu.log"; ok $rc || exit $rc
 
 timeout -k 10 400 python bench.py > "$O/bench.json" 2> "$O/bench.err"
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --filter bf16 --no-cpu-baseline --verify 2 > "$O/bench_bf16.json" 2>> "$O/bench.err"
 rc=$?; echo "bench bf16 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --config c5 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline > "$O/bench_c5.json" 2>> "$O/bench.err"
+rc=$?; echo "bench c5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --verify 0 > "$O/bench_prof.json" 2> "$O/prof.err"

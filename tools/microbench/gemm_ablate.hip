@@ -59,24 +59,16 @@ int main(int argc, char** argv) {
     // every variant stamps its in-kernel clock (STAMP): the same instantiation is not the
     // product build, whose kernels execute no stamp
     std::vector<V> vs = {
-        {"bf16 tau=inf", k_filter<OpBF16, true, 0, false, false, 2, true>, false, 1e9f, {}, {}},
-        {"bf16 tau=0.0415", k_filter<OpBF16, true, 0, false, false, 2, true>, false, 0.0415f, {}, {}},
-        {"i8 tau=inf", k_filter<OpI8, true, 0, false, false, 2, true>, true, 1e9f, {}, {}},
         {"i8 tau=0.125", k_filter<OpI8, true, 0, false, false, 2, true>, true, 0.125f, {}, {}},
-        {"i8 epi0 tau=0.125", k_filter<OpI8, true, 0, false, false, 0, true>, true, 0.125f, {}, {}},
-        {"i8 epi1 tau=0.125", k_filter<OpI8, true, 0, false, false, 1, true>, true, 0.125f, {}, {}},
-        {"i8 epi1 tau=inf", k_filter<OpI8, true, 0, false, false, 1, true>, true, 1e9f, {}, {}},
-        {"i8 no-epi", k_filter<OpI8, true, 5, false, false, 1, true>, true, 1e9f, {}, {}},
-        {"i8 no-DMA", k_filter<OpI8, true, 1, false, false, 1, true>, true, 1e9f, {}, {}},
-        {"i8 no-DMA no-epi", k_filter<OpI8, true, 6, false, false, 1, true>, true, 1e9f, {}, {}},
-        {"i8 DMA-only", k_filter<OpI8, true, 3, false, false, 1, true>, true, 1e9f, {}, {}},
-        {"qs tau=inf", k_filter_qs<true, 12, 2, true>, true, 1e9f, {}, {}, 256},
-        {"qs tau=0.125", k_filter_qs<true, 12, 2, true>, true, 0.125f, {}, {}, 256},
         {"qs2 tau=inf", k_filter_qs8<true, 12, true>, true, 1e9f, {}, {}, 512},
+        {"Qs2 tau=inf", k_filter_qs8<true, 12, false>, true, 1e9f, {}, {}, 512},
+        {"Qs2 tau=0.125", k_filter_qs8<true, 12, false>, true, 0.125f, {}, {}, 512},
+        {"Qs2 stag tau=inf", k_filter_qs8<true, 12, false, 0, true>, true, 1e9f, {}, {}, 512},
+        {"Qs2 stag tau=0.125", k_filter_qs8<true, 12, false, 0, true>, true, 0.125f, {}, {}, 512},
         {"qs2 tau=0.125", k_filter_qs8<true, 12, true>, true, 0.125f, {}, {}, 512},
-        {"Qs2 nostamp tau=inf", k_filter_qs8<true, 12, false>, true, 1e9f, {}, {}, 512},
-        {"Qs2 nostamp tau=0.125", k_filter_qs8<true, 12, false>, true, 0.125f, {}, {}, 512},
-        {"Qs nostamp tau=0.125", k_filter_qs<true, 12, 2, false>, true, 0.125f, {}, {}, 256},
+        {"Qs2 no-DMA", k_filter_qs8<true, 12, false, 1>, true, 1e9f, {}, {}, 512},
+        {"Qs2 no-epi", k_filter_qs8<true, 12, false, 5>, true, 1e9f, {}, {}, 512},
+        {"Qs2 no-DMA no-epi", k_filter_qs8<true, 12, false, 6>, true, 1e9f, {}, {}, 512},
     };
     if (only) {
         std::vector<V> keep;
