@@ -23,6 +23,8 @@ timeout -k 10 300 python bench.py --filter bf16 --no-cpu-baseline --verify 2 > "
 rc=$?; echo "bench bf16 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --config c5 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline > "$O/bench_c5.json" 2>> "$O/bench.err"
 rc=$?; echo "bench c5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline > "$O/bench_c4.json" 2>> "$O/bench.err"
+rc=$?; echo "bench c4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --verify 0 > "$O/bench_prof.json" 2> "$O/prof.err"
