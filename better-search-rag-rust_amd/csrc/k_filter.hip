@@ -516,7 +516,12 @@ __device__ __forceinline__ void qs_wait_n(int n) {
 // 0-3).
 template <bool EMIT, int NK, int NB, bool STAMP, int VAR = 0, bool STAG = false>
 __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
-    constexpr bool kNoDMA = VAR == 1 || VAR == 6, kNoEpi = VAR == 5 || VAR == 6;
+    // VAR + 8 (P - 1): one barrier per P slices (P = 2: 8-slot ring, 6 slices ahead; P = 3:
+    // 10 slots, 7 ahead; P = 3 falls back to 2 when it does not divide NK).  See the loop.
+    constexpr int kV = VAR & 7, kPr = (VAR >> 3) + 1, kP = (NK % kPr == 0) ? kPr : 2;
+    constexpr bool kNoDMA = kV == 1 || kV == 6, kNoEpi = kV == 5 || kV == 6, kB2 = kPr >= 2;
+    constexpr int kS = kP == 3 ? 10 : kQsSlots, kA = kP == 3 ? 7 : kQsAhead;
+    static_assert(!kB2 || (kS >= kA + kP && kA >= kP + 2), "ring: slot reuse and landing margins");
     // NB query blocks of 32 per wave: NB = 2 -> 4 waves x 64 queries (one wave per SIMD);
     // NB = 1 -> 8 waves x 32 queries (two per SIMD, 96 query registers each)
     constexpr int NT = 64 * (8 / NB), QW = 32 * NB;
@@ -537,10 +542,10 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     // atomics and no waits in the epilogue, the rings go to the per-query global lists once,
     // at the end (earlier if a block's rows could overfill it).
     constexpr int EM_BYTES = EMIT ? NT * NB * kQsLaneCap * 8 : 0;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[kQsSlots * kQsSlot + EM_BYTES];
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[kS * kQsSlot + EM_BYTES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds + kQsSlots * kQsSlot) + tid;
+    uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds + kS * kQsSlot) + tid;
     uint32_t ecnt[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) ecnt[n] = 0;
@@ -610,7 +615,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     };
     // DMA i (< NB) of slice jj = (iss_ti, iss_kt); the last advances the issue state
     auto issue_dma = [&](uint32_t jj, int i) {
-        uint8_t* la = lds + (jj % kQsSlots) * kQsSlot + wu * (NB * 1024) + i * 1024;
+        uint8_t* la = lds + (jj % kS) * kQsSlot + wu * (NB * 1024) + i * 1024;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma[i], iss_kt * kSliceB, 0, 0);
         if (i == NB - 1 && ++iss_kt == NK) {
             iss_kt = 0;
@@ -633,18 +638,20 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     // MFMAs have issued (one register set: the query fragments fill most of the file)
     i32x4_t fa[4][2];
     auto read_frag = [&](uint32_t jj, int m, int kk) {
-        fa[m][kk] = *reinterpret_cast<const i32x4_t*>(lds + (jj % kQsSlots) * kQsSlot + aoff[m][kk]);
+        fa[m][kk] = *reinterpret_cast<const i32x4_t*>(lds + (jj % kS) * kQsSlot + aoff[m][kk]);
     };
 
     i32x16_t acc[4][NB];
     // Prologue: slices 0..min(J, kQsAhead)-1 issued; slice 0 landed everywhere; its
     // fragments read.
     if (my_rt) set_issue_tile();
-    const uint32_t pre = J < (uint32_t)kQsAhead ? J : (uint32_t)kQsAhead;
+    const uint32_t pre = J < (uint32_t)kA ? J : (uint32_t)kA;
     for (uint32_t jj = 0; jj < pre; ++jj)
 #pragma unroll
         for (int i = 0; i < NB; ++i) issue_dma(jj, i);
-    qs_barrier(pre >= 2 ? NB * (pre - 2) : 0);  // slices 0 and 1 landed everywhere
+    // slices 0 and 1 (B2: 0, 1 and 2) landed everywhere
+    if (kB2) qs_barrier(pre >= kP + 1 ? NB * (pre - kP - 1) : 0);
+    else qs_barrier(pre >= 2 ? NB * (pre - 2) : 0);
     if (J)
 #pragma unroll
         for (int m = 0; m < 4; ++m) { read_frag(0, m, 0); read_frag(0, m, 1); }
@@ -678,10 +685,15 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     __builtin_amdgcn_sched_barrier(0);
                     read_frag(jj + 1, m, kk);  // (past the stream's end: unused; unconditional
                                                // so hipcc can count the LDS reads exactly)
-                    if (!kNoDMA && kk == 0 && (m & 1) && (m >> 1) < NB && jj + kQsAhead < J) {
+                    // B2, odd slices: the DMAs follow the slice's barrier (the slot they refill,
+                    // slice jj - 2's, is free once every wave is past it)
+                    const bool kBarSlice = kB2 && (kt % kP) == kP - 1;
+                    const bool dma_here = kBarSlice ? (kk == 1 && m >= 2 && m - 2 < NB)
+                                                             : (kk == 0 && (m & 1) && (m >> 1) < NB);
+                    if (!kNoDMA && dma_here && jj + kA < J) {
                         uint64_t ts = 0;
                         if (STAMP) ts = stamp();
-                        issue_dma(jj + kQsAhead, m >> 1);
+                        issue_dma(jj + kA, kBarSlice ? m - 2 : m >> 1);
                         if (STAMP) c_dma += stamp() - ts;
                     }
                     // Barrier: the slice after next has landed everywhere.  Younger VMEM ops
@@ -689,11 +701,29 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     // while it is younger than slice jj+2 (kt <= 3), the tile's scale load.
                     // No lgkmcnt: the slot a DMA refills next step was read two steps ago
                     // (hipcc waited for those reads before their MFMAs).
-                    if (m == 1 && kk == ((STAG && wu >= 4) ? 0 : 1)) {
+                    // P > 1: a barrier on every P-th slice only, once slices up to jj + P + 1
+                    // have landed everywhere (the reads before the next barrier, P slices on,
+                    // reach slice jj + P + 1); in flight: the DMAs of slices jj + P + 2 ..
+                    // jj + A - 1 (this slice's DMA follows the barrier) and, while younger than
+                    // slice jj + P + 1 (kt <= A - P - 2), the tile's scale load.  A DMA refills
+                    // slice jj + A - S's slot: every wave is past it (S >= A + P).
+                    if (kBarSlice && m == 1 && kk == 1) {
                         uint64_t tb = 0;
                         if (STAMP) tb = stamp();
-                        if (jj + kQsAhead < J) {
-                            qs_wait_n(NB * (kQsAhead - 2) + ((EMIT && kt <= 3) ? 1 : 0));  // (folds: kt unrolled)
+                        const int kSc = (EMIT && kt <= kA - kP - 2) ? 1 : 0;
+                        if (jj + kA < J) {
+                            qs_wait_n(NB * (kA - kP - 2) + kSc);
+                        } else if (jj + 1 < J) {
+                            const uint32_t last = J - 1;  // every DMA issued
+                            qs_barrier((last > jj + kP + 1 ? NB * (last - jj - kP - 1) : 0) + kSc);
+                        }
+                        if (STAMP) c_bar += stamp() - tb;
+                    }
+                    if (!kB2 && m == 1 && kk == ((STAG && wu >= 4) ? 0 : 1)) {
+                        uint64_t tb = 0;
+                        if (STAMP) tb = stamp();
+                        if (jj + kA < J) {
+                            qs_wait_n(NB * (kA - 2) + ((EMIT && kt <= 3) ? 1 : 0));  // (folds: kt unrolled)
                         } else if (jj + 1 < J) {  // the stream's last slices, counted at run time
                             qs_barrier((J - 1 > jj + 2 ? NB * (J - 1 - jj - 2) : 0) + ((EMIT && kt <= 3) ? 1 : 0));
                         }
@@ -1131,6 +1161,11 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// product variant of the query-stationary kernel: 8 = one barrier per two slices (B2;
+// -5% kernel time vs one per slice, profiles/r01l_*).  A/B builds override it (tools/ab).
+#ifndef BSR_QS_VAR
+#define BSR_QS_VAR 8
+#endif
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
 // query-stationary kernel; other int8 widths and bf16: k_filter.
 template <bool EMIT>
@@ -1138,12 +1173,12 @@ static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
     if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
         switch (nk) {
-            case 2: hipLaunchKernelGGL((k_filter_qs8<EMIT, 2, false>), dim3(grid), dim3(512), 0, s, a); return;
-            case 4: hipLaunchKernelGGL((k_filter_qs8<EMIT, 4, false>), dim3(grid), dim3(512), 0, s, a); return;
-            case 6: hipLaunchKernelGGL((k_filter_qs8<EMIT, 6, false>), dim3(grid), dim3(512), 0, s, a); return;
-            case 8: hipLaunchKernelGGL((k_filter_qs8<EMIT, 8, false>), dim3(grid), dim3(512), 0, s, a); return;
-            case 10: hipLaunchKernelGGL((k_filter_qs8<EMIT, 10, false>), dim3(grid), dim3(512), 0, s, a); return;
-            default: hipLaunchKernelGGL((k_filter_qs8<EMIT, 12, false>), dim3(grid), dim3(512), 0, s, a); return;
+            case 2: hipLaunchKernelGGL((k_filter_qs8<EMIT, 2, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            case 4: hipLaunchKernelGGL((k_filter_qs8<EMIT, 4, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            case 6: hipLaunchKernelGGL((k_filter_qs8<EMIT, 6, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            case 8: hipLaunchKernelGGL((k_filter_qs8<EMIT, 8, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            case 10: hipLaunchKernelGGL((k_filter_qs8<EMIT, 10, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            default: hipLaunchKernelGGL((k_filter_qs8<EMIT, 12, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
         }
     }
     if (op == kFilterI8)
