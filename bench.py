@@ -127,6 +127,9 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    # Timed region: HIP events on the filter kernels only (the roofline's launch durations);
+    # the per-stage breakdown comes from a separate profiled pass below.
+    index.set_profile(1)
     index.profile(reset=True)
     stats_fb = 0
     t0 = time.perf_counter()
@@ -136,6 +139,11 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     prof = index.profile(reset=True)
+    index.set_profile(2)
+    n_stage = max(3, min(args.steps, 10))
+    for _ in range(n_stage):
+        step()
+    prof_st = index.profile(reset=True)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -149,13 +157,19 @@ def main():
         self_ok = bool(oi[0, 0] == 0 and od[0, 0] == 0.0)
 
     # p50 single-query latency (config 4 style path: exact HBM-bound scan), all ranks.
+    # Latency without event recording; the kernel breakdown from a separate profiled pass.
     lat = []
+    index.set_profile(0)
     for _ in range(args.p50_iters):
         barrier()
         t1 = time.perf_counter()
         step(1, qdev[1:2].data_ptr())
         lat.append((time.perf_counter() - t1) * 1e3)
     p50 = statistics.median(lat) if lat else None
+    index.set_profile(2)
+    index.profile(reset=True)
+    for _ in range(max(3, min(args.p50_iters, 10))):
+        step(1, qdev[1:2].data_ptr())
     prof_scan = index.profile(reset=True)
 
     out = None
@@ -232,13 +246,13 @@ def main():
             "p50_config": f"1 query over {n_total} rows" + (
                 " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else " (exact f32 scan, HBM-bound)"),
             "roofline": roof,
-            "kernels_ms_per_step": {
-                "gemm_emit": round(prof.gemm_emit_ms / args.steps, 4),
-                "gemm_sample": round(prof.gemm_sample_ms / args.steps, 4),
-                "select": round(prof.select_ms / args.steps, 4),
-                "rescore": round(prof.rescore_ms / args.steps, 4),
-                "scan_fallback": round(prof.scan_ms / args.steps, 4),
-                "local_search_total": round(prof.search_ms / args.steps, 4),
+            "kernels_ms_per_step": {  # separate profiled pass of n_stage steps (every stage evented)
+                "gemm_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
+                "gemm_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
+                "select": round(prof_st.select_ms / n_stage, 4),
+                "rescore": round(prof_st.rescore_ms / n_stage, 4),
+                "scan_fallback": round(prof_st.scan_ms / n_stage, 4),
+                "local_search_total": round(prof_st.search_ms / n_stage, 4),
             },
             "p50_kernels_ms": {
                 "filter_emit": round(prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1), 4),

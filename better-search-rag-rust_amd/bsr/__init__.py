@@ -63,7 +63,8 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("n_queries", ctypes.c_uint32), ("n_exact_direct", ctypes.c_uint32),
                 ("n_fallback", ctypes.c_uint32), ("n_candidates", ctypes.c_uint32),
                 ("n_emitted", ctypes.c_uint64), ("filter_op", ctypes.c_uint32),
-                ("row_ebound", ctypes.c_float), ("n_rescued", ctypes.c_uint32)]
+                ("row_ebound", ctypes.c_float), ("n_rescued", ctypes.c_uint32),
+                ("graph_replay", ctypes.c_uint32)]
 
 
 class Profile(ctypes.Structure):
@@ -116,6 +117,7 @@ def lib() -> ctypes.CDLL:
         "bsr_parallel_top_k_similarity_search": (ctypes.c_int, [_P, _P, _P, u32, u32, _P, _P, _P]),
         "bsr_index_last_stats": (ctypes.c_int, [_P, ctypes.POINTER(SearchStats)]),
         "bsr_index_profile": (ctypes.c_int, [_P, ctypes.POINTER(Profile), ctypes.c_int]),
+        "bsr_index_set_profile": (ctypes.c_int, [_P, ctypes.c_int]),
         "bsr_synth_uniform": (ctypes.c_int, [_P, u64, u64, u32, u64]),
     }
     for name, (res, args) in sig.items():
@@ -302,6 +304,10 @@ class Index:
         s = SearchStats()
         _check(lib().bsr_index_last_stats(self._h, ctypes.byref(s)))
         return s
+
+    def set_profile(self, level: int) -> None:
+        """Event recording of a profiled index: 0 none, 1 filter/scan kernels, 2 every stage."""
+        _check(lib().bsr_index_set_profile(self._h, int(level)))
 
     def profile(self, reset: bool = False) -> Profile:
         p = Profile()

@@ -438,6 +438,13 @@ int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out) {
     return BSR_OK;
 }
 
+int bsr_index_set_profile(bsr_index* ix, int level) {
+    if (!ix) return set_error(BSR_E_INVALID, "null index");
+    if (level < 0 || level > 2) return set_error(BSR_E_INVALID, "profile level %d outside [0, 2]", level);
+    ix->prof_level = level;
+    return BSR_OK;
+}
+
 int bsr_index_profile(bsr_index* ix, bsr_profile* out, int reset) {
     if (!ix) return set_error(BSR_E_INVALID, "null index");
     if (out) *out = ix->prof;

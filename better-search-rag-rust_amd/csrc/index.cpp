@@ -38,9 +38,12 @@ int set_error(int code, const char* fmt, ...) {
 void clear_error() { g_err.clear(); }
 const char* last_error_cstr() { return g_err.c_str(); }
 
+std::atomic<uint64_t> g_alloc_gen{0};
+
 int DevBuf::ensure(size_t need) {
     if (need <= bytes && p) return BSR_OK;
     release();
+    ++g_alloc_gen;
     if (need == 0) need = 16;
     hipError_t e = hipMalloc(&p, need);
     if (e != hipSuccess) {
@@ -99,12 +102,20 @@ using namespace bsr;
 // ---------------------------------------------------------------------------------------
 // profiling helpers
 // ---------------------------------------------------------------------------------------
+// Events exist when the index was created with BSR_FLAG_PROFILE; prof_level (bsr_index_set_profile)
+// picks which stages record them: 1 = the filter / scan kernels only, 2 = every stage.
 static inline bool profiling(const bsr_index* ix) { return (ix->cfg.flags & BSR_FLAG_PROFILE) != 0; }
-static inline void ev_begin(bsr_index* ix, Events& e) {
-    if (profiling(ix) && e.a) { (void)hipEventRecord(e.a, ix->stream); e.armed = true; }
+static inline void ev_begin(bsr_index* ix, Events& e, int level = 2) {
+    if (profiling(ix) && ix->prof_level >= level && e.a) { (void)hipEventRecord(e.a, ix->stream); e.armed = true; }
 }
 static inline void ev_end(bsr_index* ix, Events& e) {
     if (profiling(ix) && e.armed) (void)hipEventRecord(e.b, ix->stream);
+}
+// Events of one filter / scan kernel: handed to its launch (hipExtLaunchKernel records them at
+// the kernel's own dispatch and completion), so they time the kernel, not the stream gaps.
+static inline void ev_kernel(bsr_index* ix, Events& e, hipEvent_t& a, hipEvent_t& b) {
+    a = b = nullptr;
+    if (profiling(ix) && ix->prof_level >= 1 && e.a) { a = e.a; b = e.b; e.armed = true; }
 }
 static inline void ev_collect(Events& e, double& ms, uint64_t& n, uint64_t launches) {
     if (!e.armed) return;
@@ -199,6 +210,12 @@ int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
     return BSR_OK;
 }
 
+bsr_index::~bsr_index() {
+    for (SearchGraph& g : graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (h_res) (void)hipHostFree(h_res);
+}
+
 void bsr_index_destroy_impl(bsr_index* ix) {
     if (!ix) return;
     (void)hipSetDevice(ix->device);
@@ -271,7 +288,7 @@ static int run_exact_scan(bsr_index* ix, const int32_t* ids, uint32_t n_ids, uin
     const uint32_t groups = (n_ids + kScanQF - 1) / kScanQF;
     const uint32_t grid = scan_grid_for(ix->n);
     BSR_TRY(ix->part.ensure((size_t)grid * kScanQF * k * sizeof(uint64_t)));
-    ev_begin(ix, ix->ev_scan);
+    ev_begin(ix, ix->ev_scan, 1);
     for (uint32_t g = 0; g < groups; ++g) {
         const uint32_t nqf = std::min(kScanQF, n_ids - g * kScanQF);
         const int32_t* qid = ids + (size_t)g * kScanQF;
@@ -351,10 +368,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         g.S = ix->S.as<float>();
         g.s_ld = s_ld;
         g.s_compact = compact ? 1u : 0u;
-        ev_begin(ix, ix->ev_sample);
-        if (skinny) BSR_HIP(launch_filter_skinny_sample(g, ix->stream));
-        else BSR_HIP(launch_filter_sample(ix->op, g, ix->stream));
-        ev_end(ix, ix->ev_sample);
+        hipEvent_t e0, e1;
+        ev_kernel(ix, ix->ev_sample, e0, e1);
+        if (skinny) BSR_HIP(launch_filter_skinny_sample(g, ix->stream, e0, e1));
+        else BSR_HIP(launch_filter_sample(ix->op, g, ix->stream, e0, e1));
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
                                   ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
     } else {
@@ -370,10 +387,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cand = ix->cand.as<uint64_t>();
     g.cnt = ix->cnt.as<uint32_t>();
     g.cap = cap;
-    ev_begin(ix, ix->ev_emit);
-    if (skinny) BSR_HIP(launch_filter_skinny_emit(g, ix->stream));
-    else BSR_HIP(launch_filter_emit(ix->op, g, ix->stream));
-    ev_end(ix, ix->ev_emit);
+    hipEvent_t e0, e1;
+    ev_kernel(ix, ix->ev_emit, e0, e1);
+    if (skinny) BSR_HIP(launch_filter_skinny_emit(g, ix->stream, e0, e1));
+    else BSR_HIP(launch_filter_emit(ix->op, g, ix->stream, e0, e1));
     ev_begin(ix, ix->ev_select);
     BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(), kp,
                                ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), ix->tau_excl.as<float>(),
@@ -430,6 +447,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         h_res_bytes = 0;
         BSR_HIP(hipHostMalloc((void**)&h_res, res_bytes, hipHostMallocDefault));
         h_res_bytes = res_bytes;
+        ++g_alloc_gen;
     }
     cur ^= 1u;
     uint8_t* rb = res[cur].as<uint8_t>();
@@ -482,30 +500,71 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     qa.qids = qids_id.as<int32_t>();
     qa.status = d_status;
     qa.with_op = use_filter;
-    BSR_HIP(launch_query_prep(qa, stream));
+    // prep -> local search -> finalize -> one D2H copy of the packed result (graph-capturable:
+    // no allocation and no host synchronisation once the buffers are sized)
+    auto enqueue_search = [&]() -> int {
+        BSR_HIP(launch_query_prep(qa, stream));
+        if (n == 0) {
+            // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
+            BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
+        } else if (!use_filter) {
+            stats.n_exact_direct = nq;
+            BSR_TRY(run_exact_scan(ix, qids_id.as<int32_t>(), nq, k));
+        } else {
+            BSR_TRY(run_filter(ix, nq, qpad, k));
+        }
+        BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
+                                stream));
+        ev_end(ix, ev_total);
+        BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
+        return BSR_OK;
+    };
 
-    std::vector<int32_t> exact_ids;
-    if (n == 0) {
-        // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
-        BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
-    } else if (!use_filter) {
-        stats.n_exact_direct = nq;
-        BSR_TRY(run_exact_scan(ix, qids_id.as<int32_t>(), nq, k));
+    const bool graphable = use_filter && n > 0 && nq <= kSkinnyMaxQ && (!profiling(ix) || prof_level == 0);
+    SearchGraph& gs = graphs[cur];
+    const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n;
+    if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen) {
+        BSR_HIP(hipGraphLaunch(gs.exec, stream));
+        stats.n_candidates = kp_for(k);
+        ++graph_replays;
+        stats.graph_replay = 1;
+    } else if (graphable && same_shape && warm.gen == g_alloc_gen) {
+        // capture (every buffer already sized by the direct search of this shape), then replay
+        if (gs.exec) { (void)hipGraphExecDestroy(gs.exec); gs.exec = nullptr; }
+        BSR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        const uint64_t gen0 = g_alloc_gen;
+        const int rc = enqueue_search();
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(stream, &graph);
+        if (rc != BSR_OK) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+        if (ec != hipSuccess || g_alloc_gen != gen0) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return set_error(BSR_E_HIP, "search graph capture failed: %s", hipGetErrorString(ec));
+        }
+        hipGraphExec_t exec = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return set_error(BSR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen};
+        BSR_HIP(hipGraphLaunch(gs.exec, stream));
+        ++graph_replays;
+        stats.graph_replay = 1;
     } else {
-        BSR_TRY(run_filter(ix, nq, qpad, k));
+        BSR_TRY(enqueue_search());
+        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen};
     }
-    // Finalize into the packed result and read it back with ONE copy: status words
-    // (non-finite queries, uncertified queries) and the lists.
+    next_status_clean = true;
+    BSR_HIP(hipStreamSynchronize(stream));
+    // Later rounds (second-chance rescore, scan) finalize and read back again, directly.
     auto finalize_and_read = [&]() -> int {
         BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
                                 stream));
         next_status_clean = true;
-        ev_end(ix, ev_total);
         BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
         BSR_HIP(hipStreamSynchronize(stream));
         return BSR_OK;
     };
-    BSR_TRY(finalize_and_read());
+    std::vector<int32_t> exact_ids;
     const uint32_t* st = reinterpret_cast<const uint32_t*>(h_res);
     if (st[kStQueryFlags] & kQueryNonFinite) {
         h_qflags.resize(nq);

@@ -5,6 +5,8 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include <string>
 #include <vector>
 
@@ -29,6 +31,10 @@ void clear_error();
         int r_ = (call);            \
         if (r_ != BSR_OK) return r_; \
     } while (0)
+
+// Bumped by every device / pinned (re)allocation: a captured search graph is valid only
+// for the generation it was captured in.
+extern std::atomic<uint64_t> g_alloc_gen;
 
 // Growable device allocation (never shrinks).
 struct DevBuf {
@@ -90,12 +96,28 @@ struct bsr_index {
     uint32_t* d_cnt = nullptr;
     float* d_dist = nullptr;
     uint64_t* d_idx = nullptr;
-    ~bsr_index() { if (h_res) (void)hipHostFree(h_res); }
+
     std::vector<uint32_t> h_qflags, h_fail;
 
     bsr_search_stats stats{};
     bsr_profile prof{};
     bsr::Events ev_emit, ev_sample, ev_select, ev_rescore, ev_scan, ev_total;
+    int prof_level = 2;  // bsr_index_set_profile
+
+    // Small filtered batches (<= kSkinnyMaxQ queries, the latency path) replay a captured
+    // hipGraph of query prep -> filter -> select -> rescore -> finalize -> D2H instead of
+    // ~9 launches.  One graph per result buffer; captured on the second search of a shape
+    // (the first sizes every buffer), dropped when the shape or any allocation changes.
+    struct SearchGraph {
+        hipGraphExec_t exec = nullptr;
+        uint32_t nq = 0, k = 0;
+        const float* qsrc = nullptr;
+        uint64_t n = 0, gen = 0;
+    };
+    SearchGraph graphs[2];
+    SearchGraph warm;  // the last direct search of a graphable shape (no exec)
+    uint64_t graph_replays = 0;
+    ~bsr_index();
 
     // Run the local search; results stay in d_idx / d_dist / d_cnt (device, [nq][k]) and in
     // the pinned host mirror h_res at the same offsets.

@@ -15,6 +15,8 @@
 #include "bsr_device.hpp"
 #include "kernels.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <math.h>
 
 #include <algorithm>
@@ -1135,29 +1137,37 @@ static uint32_t filter_grid(uint32_t n_qt) {
     return 8 * per_xcd;
 }
 
+// Filter launches: with timing events, hipExtLaunchKernel records them at the kernel's own
+// dispatch and completion; without, a plain launch (also inside stream capture).
+#define BSR_KLAUNCH(K, G, B, S, E0, E1, A)                               \
+    do {                                                                 \
+        if (E0) hipExtLaunchKernelGGL(K, G, B, 0, S, E0, E1, 0u, A);     \
+        else hipLaunchKernelGGL(K, G, B, 0, S, A);                       \
+    } while (0)
+
 static uint32_t skinny_grid(uint32_t n_rows) {
     const uint32_t groups = (n_rows + 31) / 32, wgs = (groups + 3) / 4;
     return wgs < 768 ? (wgs ? wgs : 1) : 768;  // 3 workgroups per CU (VGPR-limited occupancy)
 }
 // v2 for rows of <= 16 K steps (1024 int8), v1 beyond.
 template <bool EMIT>
-static void launch_skinny(const GemmArgs& a, hipStream_t s) {
+static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB;
     // v2 holds ~170 VGPRs: 2 waves per SIMD = 2 workgroups per CU
     const uint32_t units = (a.n_rows + 15) / 16, g2 = std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
     const dim3 g(nk <= 16 ? g2 : skinny_grid(a.n_rows)), b(256);
-    if (nk <= 4) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 4>), g, b, 0, s, a);
-    else if (nk <= 8) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 8>), g, b, 0, s, a);
-    else if (nk <= 12) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 12>), g, b, 0, s, a);
-    else if (nk <= 16) hipLaunchKernelGGL((k_filter_skinny2<EMIT, 16>), g, b, 0, s, a);
-    else hipLaunchKernelGGL(k_filter_skinny<EMIT>, g, b, 0, s, a);
+    if (nk <= 4) BSR_KLAUNCH((k_filter_skinny2<EMIT, 4>), g, b, s, e0, e1, a);
+    else if (nk <= 8) BSR_KLAUNCH((k_filter_skinny2<EMIT, 8>), g, b, s, e0, e1, a);
+    else if (nk <= 12) BSR_KLAUNCH((k_filter_skinny2<EMIT, 12>), g, b, s, e0, e1, a);
+    else if (nk <= 16) BSR_KLAUNCH((k_filter_skinny2<EMIT, 16>), g, b, s, e0, e1, a);
+    else BSR_KLAUNCH(k_filter_skinny<EMIT>, g, b, s, e0, e1, a);
 }
-hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s) {
-    launch_skinny<false>(a, s);
+hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_skinny<false>(a, s, e0, e1);
     return hipGetLastError();
 }
-hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
-    launch_skinny<true>(a, s);
+hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_skinny<true>(a, s, e0, e1);
     return hipGetLastError();
 }
 
@@ -1169,29 +1179,29 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s) {
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
 // query-stationary kernel; other int8 widths and bf16: k_filter.
 template <bool EMIT>
-static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s) {
+static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
     if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
         switch (nk) {
-            case 2: hipLaunchKernelGGL((k_filter_qs8<EMIT, 2, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
-            case 4: hipLaunchKernelGGL((k_filter_qs8<EMIT, 4, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
-            case 6: hipLaunchKernelGGL((k_filter_qs8<EMIT, 6, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
-            case 8: hipLaunchKernelGGL((k_filter_qs8<EMIT, 8, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
-            case 10: hipLaunchKernelGGL((k_filter_qs8<EMIT, 10, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
-            default: hipLaunchKernelGGL((k_filter_qs8<EMIT, 12, false, BSR_QS_VAR>), dim3(grid), dim3(512), 0, s, a); return;
+            case 2: BSR_KLAUNCH((k_filter_qs8<EMIT, 2, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            case 4: BSR_KLAUNCH((k_filter_qs8<EMIT, 4, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            case 6: BSR_KLAUNCH((k_filter_qs8<EMIT, 6, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            case 8: BSR_KLAUNCH((k_filter_qs8<EMIT, 8, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            case 10: BSR_KLAUNCH((k_filter_qs8<EMIT, 10, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            default: BSR_KLAUNCH((k_filter_qs8<EMIT, 12, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
         }
     }
     if (op == kFilterI8)
-        hipLaunchKernelGGL((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), 0, s, a);
+        BSR_KLAUNCH((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
     else
-        hipLaunchKernelGGL((k_filter<OpBF16, EMIT>), dim3(grid), dim3(kThreads), 0, s, a);
+        BSR_KLAUNCH((k_filter<OpBF16, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
 }
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s) {
-    launch_filter<false>(op, a, s);
+hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_filter<false>(op, a, s, e0, e1);
     return hipGetLastError();
 }
-hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s) {
-    launch_filter<true>(op, a, s);
+hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_filter<true>(op, a, s, e0, e1);
     return hipGetLastError();
 }
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,

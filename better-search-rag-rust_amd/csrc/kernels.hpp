@@ -91,13 +91,17 @@ struct GemmArgs {
     uint32_t* cnt;          // emit: [qpad] counters
     uint32_t cap;
 };
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s);
-hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s);
+// e0 / e1 (optional): events recorded at the kernel's own dispatch and completion
+// (hipExtLaunchKernel), i.e. its device duration without the stream's launch gaps.
+hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+                                hipEvent_t e1 = nullptr);
+hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+                              hipEvent_t e1 = nullptr);
 // int8 only, batches of <= 16 queries (query tile rows 0..15), HBM-bound: the same
 // contract as the two launches above.
 constexpr uint32_t kSkinnyMaxQ = 16;
-hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s);
-hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s);
+hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // tau[q] = the ks-th best sampled score; also zeroes cnt[0..qpad) and the status words
 // kStFail / kStEmitted for the emit pass that follows.

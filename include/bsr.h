@@ -89,6 +89,7 @@ typedef struct {
     uint32_t filter_op;        /* 0 = int8 filter, 1 = bf16 filter (BSR_FLAG_FILTER_BF16) */
     float row_ebound;          /* int8: max over rows of ||a/|a| - s q||_2 (0 for bf16) */
     uint32_t n_rescued;        /* queries certified by the second chance (all emitted rows) */
+    uint32_t graph_replay;     /* 1: the search replayed a captured hipGraph (small batches) */
 } bsr_search_stats;
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts
@@ -171,6 +172,9 @@ int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const fl
 /* ---- diagnostics ------------------------------------------------------------------ */
 int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out);
 int bsr_index_profile(bsr_index* ix, bsr_profile* out, int reset);
+/* Which stages of a BSR_FLAG_PROFILE index record HIP events: 0 = none (latency runs),
+ * 1 = the filter / scan kernels only, 2 = every stage (the default). */
+int bsr_index_set_profile(bsr_index* ix, int level);
 
 /* ---- synthetic data (bench / tests): U(-1,1) f32 from a counter-based hash of
  * (seed, global element index), written on the device: value(row, col) for rows

@@ -356,3 +356,38 @@ def test_device_pointer_inputs(bsr_mod, oracle_mod, gpu):
     ix.local_top_k_device(dq, 33, 10, oi, od, oc)
     got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "device ptrs")
+
+
+# ---- captured search graphs (small batches replay one hipGraph) ---------------------------
+def test_small_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu):
+    """Batches of <= 16 queries replay a captured graph from their third search of a shape on;
+    every replay must read the queries of ITS call (host staging and device pointers), and
+    shape changes must not replay a stale graph."""
+    import torch
+    rng = np.random.default_rng(21)
+    rows = rng.uniform(-1, 1, (40000, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=64)
+    replays = 0
+    for it in range(8):
+        for nq, k in ((1, 10), (1, 10), (3, 10), (1, 25)):
+            qs = rng.uniform(-1, 1, (nq, 768)).astype(np.float32)
+            qs[0] = rows[(it * 7919) % len(rows)]
+            got = ix.local_top_k(qs, k)
+            replays += ix.last_stats().graph_replay
+            _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"host it={it} nq={nq} k={k}")
+    assert replays > 0
+    # device-pointer queries: same buffer, contents rewritten between searches
+    dq = torch.empty((2, 768), dtype=torch.float32, device="cuda:0")
+    oi = torch.empty((2, 10), dtype=torch.int64, device="cuda:0")
+    od = torch.empty((2, 10), dtype=torch.float32, device="cuda:0")
+    oc = torch.empty(2, dtype=torch.int32, device="cuda:0")
+    dev_replays = 0
+    for it in range(6):
+        qs = rng.uniform(-1, 1, (2, 768)).astype(np.float32)
+        dq.copy_(torch.from_numpy(qs))
+        torch.cuda.synchronize()
+        ix.local_top_k_device(dq, 2, 10, oi, od, oc)
+        dev_replays += ix.last_stats().graph_replay
+        got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
+        _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), f"device it={it}")
+    assert dev_replays > 0
