@@ -520,7 +520,12 @@ template <bool EMIT, int NK, int NB, bool STAMP, int VAR = 0, bool STAG = false>
 __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     // VAR + 8 (P - 1): one barrier per P slices (P = 2: 8-slot ring, 6 slices ahead; P = 3:
     // 10 slots, 7 ahead; P = 3 falls back to 2 when it does not divide NK).  See the loop.
-    constexpr int kV = VAR & 7, kPr = (VAR >> 3) + 1, kP = (NK % kPr == 0) ? kPr : 2;
+    constexpr int kV = VAR & 7, kPr = ((VAR >> 3) & 7) + 1, kP = (NK % kPr == 0) ? kPr : 2;
+    // VAR + 64 (P > 1 only): steady DMA stream -- the DMAs never stop early (slices past the
+    // end re-read the last tile into slots nobody reads again), so every wait is the
+    // steady-state count and hipcc sees the same number of VMEM ops on every path (its own
+    // wait for the tile's scale load is then not a full drain).  Drained before exit.
+    constexpr bool kSteady = (VAR & 64) != 0 && kPr >= 2;
     constexpr bool kNoDMA = kV == 1 || kV == 6, kNoEpi = kV == 5 || kV == 6, kB2 = kPr >= 2;
     constexpr int kS = kP == 3 ? 10 : kQsSlots, kA = kP == 3 ? 7 : kQsAhead;
     static_assert(!kB2 || (kS >= kA + kP && kA >= kP + 2), "ring: slot reuse and landing margins");
@@ -647,7 +652,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     // Prologue: slices 0..min(J, kQsAhead)-1 issued; slice 0 landed everywhere; its
     // fragments read.
     if (my_rt) set_issue_tile();
-    const uint32_t pre = J < (uint32_t)kA ? J : (uint32_t)kA;
+    const uint32_t pre = kSteady ? (J ? (uint32_t)kA : 0u) : (J < (uint32_t)kA ? J : (uint32_t)kA);
     for (uint32_t jj = 0; jj < pre; ++jj)
 #pragma unroll
         for (int i = 0; i < NB; ++i) issue_dma(jj, i);
@@ -692,7 +697,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     const bool kBarSlice = kB2 && (kt % kP) == kP - 1;
                     const bool dma_here = kBarSlice ? (kk == 1 && m >= 2 && m - 2 < NB)
                                                              : (kk == 0 && (m & 1) && (m >> 1) < NB);
-                    if (!kNoDMA && dma_here && jj + kA < J) {
+                    if (!kNoDMA && dma_here && (kSteady || jj + kA < J)) {
                         uint64_t ts = 0;
                         if (STAMP) ts = stamp();
                         issue_dma(jj + kA, kBarSlice ? m - 2 : m >> 1);
@@ -713,7 +718,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                         uint64_t tb = 0;
                         if (STAMP) tb = stamp();
                         const int kSc = (EMIT && kt <= kA - kP - 2) ? 1 : 0;
-                        if (jj + kA < J) {
+                        if (kSteady ? jj + 1 < J : jj + kA < J) {
                             qs_wait_n(NB * (kA - kP - 2) + kSc);
                         } else if (jj + 1 < J) {
                             const uint32_t last = J - 1;  // every DMA issued
@@ -813,6 +818,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
         if (stored) wait_vm0();
         if (STAMP) c_epi += stamp() - te;
     }
+    if (kSteady) wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
     if constexpr (EMIT) {
 #pragma unroll
         for (int n = 0; n < NB; ++n) flush_ring(n);
@@ -1172,9 +1178,11 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 }
 
 // product variant of the query-stationary kernel: 8 = one barrier per two slices (B2;
-// -5% kernel time vs one per slice, profiles/r01l_*).  A/B builds override it (tools/ab).
+// -5% kernel time vs one per slice, profiles/r01l_*), + 64 = steady DMA stream (no full
+// vmcnt drain at each tile's epilogue; -1.5%, profiles/r01n_*).  A/B builds override it
+// (tools/ab).
 #ifndef BSR_QS_VAR
-#define BSR_QS_VAR 8
+#define BSR_QS_VAR 72
 #endif
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
 // query-stationary kernel; other int8 widths and bf16: k_filter.

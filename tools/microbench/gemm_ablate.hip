@@ -74,6 +74,9 @@ int main(int argc, char** argv) {
         {"b2 tau=0.125", k_filter_qs8<true, 12, true, 8>, true, 0.125f, {}, {}, 512},
         {"B2 no-epi", k_filter_qs8<true, 12, false, 13>, true, 1e9f, {}, {}, 512},
         {"B2 no-DMA no-epi", k_filter_qs8<true, 12, false, 14>, true, 1e9f, {}, {}, 512},
+        {"S2 tau=inf", k_filter_qs8<true, 12, false, 72>, true, 1e9f, {}, {}, 512},
+        {"S2 tau=0.125", k_filter_qs8<true, 12, false, 72>, true, 0.125f, {}, {}, 512},
+        {"S2 no-epi", k_filter_qs8<true, 12, false, 77>, true, 1e9f, {}, {}, 512},
         {"B3 tau=inf", k_filter_qs8<true, 12, false, 16>, true, 1e9f, {}, {}, 512},
         {"B3 tau=0.125", k_filter_qs8<true, 12, false, 16>, true, 0.125f, {}, {}, 512},
         {"B3 no-epi", k_filter_qs8<true, 12, false, 21>, true, 1e9f, {}, {}, 512},
