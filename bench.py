@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--p50-iters", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed searches before the warmup steps (setup): the GPU leaves its idle "
+                         "clocks only after some ms of load, longer than a few warmup steps take")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle (rank 0, N=1)")
@@ -124,6 +127,9 @@ def main():
         if st != 0:
             raise bsr.BsrError(st, lib.bsr_last_error().decode())
 
+    t_settle = time.perf_counter() + args.settle_ms * 1e-3
+    while time.perf_counter() < t_settle:
+        step()
     for _ in range(args.warmup):
         step()
     barrier()
@@ -222,6 +228,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
