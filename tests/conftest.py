@@ -25,6 +25,13 @@ def oracle_mod():
 
 @pytest.fixture(scope="session")
 def bsr_mod():
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64, so it is loaded
+    # before libbsr.so pulls in /opt/rocm's (torch imported after the library has used HIP
+    # reports no GPUs; tools/diag/torch_after_graph.py).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     import bsr
     bsr.lib()  # raises if libbsr.so is missing: no fallback
     return bsr

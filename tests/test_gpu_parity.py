@@ -391,3 +391,25 @@ def test_small_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu):
         got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
         _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), f"device it={it}")
     assert dev_replays > 0
+
+
+def test_profile_levels(bsr_mod, oracle_mod, gpu):
+    """bsr_index_set_profile: level 1 times only the filter kernels (events bound to their
+    dispatch), 2 every stage, 0 none -- results identical at every level."""
+    rng = np.random.default_rng(31)
+    rows = rng.uniform(-1, 1, (30000, 768)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (40, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=16, flags=bsr_mod.BSR_FLAG_PROFILE)
+    want = oracle_mod.parallel_top_k(rows, qs, 10)
+    seen = {}
+    for level in (2, 1, 0):
+        ix.set_profile(level)
+        ix.profile(reset=True)
+        _assert_same(ix.local_top_k(qs, 10), want, f"level {level}")
+        seen[level] = ix.profile(reset=True)
+    assert seen[2].gemm_emit_launches == 1 and seen[2].select_launches == 1 and seen[2].searches == 1
+    assert seen[1].gemm_emit_launches == 1 and seen[1].select_launches == 0 and seen[1].searches == 0
+    assert seen[1].gemm_emit_ms > 0.0
+    assert seen[0].gemm_emit_launches == 0 and seen[0].searches == 0
+    with pytest.raises(bsr_mod.BsrError):
+        ix.set_profile(3)
