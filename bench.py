@@ -127,8 +127,17 @@ def main():
         if st != 0:
             raise bsr.BsrError(st, lib.bsr_last_error().decode())
 
-    t_settle = time.perf_counter() + args.settle_ms * 1e-3
-    while time.perf_counter() < t_settle:
+    # Clock settle: the same number of untimed searches on every rank (each search is a
+    # collective for N > 1), sized on rank 0 from one search's time.
+    step()
+    t1 = time.perf_counter()
+    step()
+    n_settle = int(args.settle_ms * 1e-3 / max(time.perf_counter() - t1, 1e-5)) if args.settle_ms > 0 else 0
+    if dist:
+        nt = torch.tensor([n_settle], dtype=torch.int64)
+        dist.broadcast(nt, src=0)
+        n_settle = int(nt.item())
+    for _ in range(n_settle):
         step()
     for _ in range(args.warmup):
         step()
