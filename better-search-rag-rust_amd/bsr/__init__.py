@@ -600,6 +600,44 @@ def get_local_vstore(vstore_dir: str, rank: int, empty: bool) -> PolarsVectorsto
     return PolarsVectorstore(buf.value.decode(), empty)
 
 
+def merge_vector_stores(size: int, vstore_dir: str) -> PolarsVectorstore:
+    """src/mpi_helpers/tasks.rs:181-217: an empty global store, then every rank's local store
+    appended in rank order (empty ones skipped); the order defines the global row indices the
+    search returns.  Like the reference, the merged store is returned, not persisted."""
+    global_vs = get_global_vstore(vstore_dir, True)
+    total = 0
+    for r in range(size):
+        local = get_local_vstore(vstore_dir, r, False)
+        try:
+            n = local.get_count()
+            if n == 0:
+                continue
+            rows = local.get_many_array(None, dim=len(local.get(0)))
+            global_vs.append_many(rows)
+            total += rows.shape[0]
+        finally:
+            local.close()
+    return global_vs
+
+
+def merge_vector_stores_into_index(index: "Index", size: int, vstore_dir: str) -> int:
+    """f-3 on the device: the rank-order concatenation of merge_vector_stores built directly
+    as a GPU-resident shard (each local store's rows appended to the index's HBM slab with
+    bsr_index_append), without materialising the global parquet store.  Returns the row count."""
+    total = 0
+    for r in range(size):
+        local = get_local_vstore(vstore_dir, r, False)
+        try:
+            n = local.get_count()
+            if n == 0:
+                continue
+            index.append_many(local.get_many_array(None, dim=index.dim))
+            total += n
+        finally:
+            local.close()
+    return total
+
+
 def load_index_from_vstore(index: "Index", vstore: PolarsVectorstore, rank: int, size: int) -> None:
     """The read half of compute_local_top_k (src/mpi_helpers/metrics.rs:23-33): this rank's
     interval_by_rank block of the store, straight into the index's HBM shard."""

@@ -181,3 +181,41 @@ def test_index_load_vstore_blocks_search_like_reference(bsr_mod, oracle_mod, gpu
     wi, wd, wc = oracle_mod.parallel_top_k(data, qs, k, size=P)
     assert np.array_equal(got[2], wc) and np.array_equal(got[0], wi)
     assert np.array_equal(got[1].view(np.uint32), wd.view(np.uint32))
+
+
+# ---- f-3: src/mpi_helpers/tasks.rs:181-217 (merge_vector_stores) ------------------------
+def _write_local_stores(bsr_mod, tmp_path, rng, counts):
+    parts = []
+    for r, n in enumerate(counts):
+        vs = bsr_mod.get_local_vstore(tmp_path, r, True)
+        rows = mock_embeddings(rng, n)
+        if n:
+            vs.append_many(rows)
+        vs.persist()
+        vs.close()
+        parts.append(rows)
+    return np.concatenate(parts)
+
+
+def test_merge_vector_stores_rank_order_skips_empty(bsr_mod, tmp_path, rng):
+    want = _write_local_stores(bsr_mod, tmp_path, rng, [5, 0, 7, 3])  # rank 1 empty (skipped)
+    merged = bsr_mod.merge_vector_stores(4, tmp_path)
+    assert merged.get_count() == 15
+    assert np.array_equal(merged.get_many_array(None, DIMENSION), want)
+    assert merged.path.endswith("global.parquet")
+    merged.close()
+
+
+@pytest.mark.gpu
+def test_merge_vector_stores_into_index_matches_host_merge(bsr_mod, oracle_mod, gpu, tmp_path, rng):
+    want = _write_local_stores(bsr_mod, tmp_path, rng, [900, 0, 1300, 451])
+    ix = bsr_mod.Index(DIMENSION, max_k=16, device=0)
+    assert bsr_mod.merge_vector_stores_into_index(ix, 4, tmp_path) == len(want)
+    assert ix.get_count() == len(want)
+    qs = mock_embeddings(rng, 5)
+    qs[0] = want[1000]
+    got = ix.local_top_k(qs, 10)
+    wi, wd, wc = oracle_mod.parallel_top_k(want, qs, 10)
+    assert np.array_equal(got[2], wc) and np.array_equal(got[0], wi)
+    assert np.array_equal(got[1].view(np.uint32), wd.view(np.uint32))
+    assert got[0][0, 0] == 1000
