@@ -442,6 +442,50 @@ def calculate_accuracy_metrics(top_k_results, query_idx: int, top_k: int):
     return mrr, recall, overlap
 
 
+def print_top_k_results(top_k_results, out=None) -> None:
+    """src/mpi_helpers/metrics.rs:209-214 (Rust's `{}` of an f32 is its shortest round-trip
+    form, as Python's repr of the same float32)."""
+    import sys as _sys
+    w = (out or _sys.stdout).write
+    w(f"Global top-{len(top_k_results)} results:\n")
+    for i, (idx, dist) in enumerate(top_k_results):
+        w(f"  {i + 1}. Index: {idx}, Distance: {_rust_f32(dist)}\n")
+
+
+def _rust_f32(x) -> str:
+    """Rust's Display of an f32: the shortest round-trip digits, positional, no exponent."""
+    return np.format_float_positional(np.float32(x), unique=True, trim="-")
+
+
+def run_search_stage(world, rank: int, size: int, index: "Index", target_vector=None, top_k: int = 50,
+                     query_idx: int = 0, out=None):
+    """The driver's search stage (src/main.rs:109-163): query = row `query_idx` of rank 0's
+    store (broadcast by the caller as `target_vector`, or read from the index), the parallel
+    top-k search timed as "similarity_search", then on the root the result list and the
+    accuracy metrics printed in the reference's format.  Returns (results, metrics,
+    seconds) on the root, (None, None, seconds) elsewhere."""
+    import sys as _sys
+    import time as _time
+    w = (out or _sys.stdout).write
+    if target_vector is None:
+        target_vector = index.get(query_idx)
+    t0 = _time.perf_counter()
+    res = parallel_top_k_similarity_search(world, rank, size, index, top_k, target_vector)
+    secs = _time.perf_counter() - t0
+    if rank != ROOT:
+        return None, None, secs
+    if res is None:
+        w("Error: Failed to compute global top-k results\n")
+        return None, None, secs
+    print_top_k_results(res, out)
+    mrr, recall, overlap = calculate_accuracy_metrics(res, query_idx, top_k)
+    w("Accuracy Metrics:\n")
+    w(f"  Mean Reciprocal Rank (MRR): {mrr:.4f}\n")
+    w(f"  Recall@{top_k}: {recall:.4f}\n")
+    w(f"  Top-k Overlap: {overlap:.4f}\n")
+    return res, (mrr, recall, overlap), secs
+
+
 def synth_uniform(dev_ptr: int, row0: int, n_rows: int, dim: int, seed: int):
     """Fill device memory with the synthetic U(-1,1) corpus rows [row0, row0+n_rows)."""
     _check(lib().bsr_synth_uniform(dev_ptr, row0, n_rows, dim, seed))

@@ -413,3 +413,23 @@ def test_profile_levels(bsr_mod, oracle_mod, gpu):
     assert seen[0].gemm_emit_launches == 0 and seen[0].searches == 0
     with pytest.raises(bsr_mod.BsrError):
         ix.set_profile(3)
+
+
+def test_driver_search_stage_reference_report(bsr_mod, oracle_mod, gpu):
+    """src/main.rs:109-163: query = row 0, k = 50, the result list and the accuracy metrics
+    printed in the reference's format; the self-query ranks first (MRR = recall = overlap = 1)."""
+    import io
+    rng = np.random.default_rng(50)
+    rows = rng.uniform(-1, 1, (12000, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=64)
+    buf = io.StringIO()
+    res, metrics, secs = bsr_mod.run_search_stage(None, 0, 1, ix, top_k=50, out=buf)
+    wi, wd, wc = oracle_mod.parallel_top_k(rows, rows[:1], 50)
+    assert [i for i, _ in res] == list(wi[0, :wc[0]])
+    assert np.array_equal(np.array([d for _, d in res], np.float32).view(np.uint32), wd[0, :wc[0]].view(np.uint32))
+    assert metrics == (1.0, 1.0, 1.0) and secs > 0
+    lines = buf.getvalue().splitlines()
+    assert lines[0] == "Global top-50 results:"
+    assert lines[1] == "  1. Index: 0, Distance: 0"
+    assert lines[-4:] == ["Accuracy Metrics:", "  Mean Reciprocal Rank (MRR): 1.0000", "  Recall@50: 1.0000",
+                          "  Top-k Overlap: 1.0000"]

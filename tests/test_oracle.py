@@ -86,3 +86,16 @@ def test_golden_search_reproduces(oracle_mod):
         assert np.array_equal(cnt, g[f"c{ci}_count"])
         assert np.array_equal(idx, g[f"c{ci}_idx"])
         assert np.array_equal(dist.view(np.uint32), g[f"c{ci}_dist_bits"])
+
+
+def test_print_top_k_results_reference_format(bsr_mod):
+    """src/mpi_helpers/metrics.rs:209-214 with Rust's f32 Display (shortest round trip, positional)."""
+    import io
+    buf = io.StringIO()
+    bsr_mod.print_top_k_results([(0, np.float32(0.0)), (17, np.float32(0.83125)), (3, np.float32(1e-8)),
+                                 (9, np.float32(1.0))], out=buf)
+    assert buf.getvalue().splitlines() == ["Global top-4 results:", "  1. Index: 0, Distance: 0",
+                                           "  2. Index: 17, Distance: 0.83125", "  3. Index: 3, Distance: 0.00000001",
+                                           "  4. Index: 9, Distance: 1"]
+    assert bsr_mod.calculate_accuracy_metrics([(4, 0.0), (0, 0.1)], 0, 50) == (0.5, 1.0, 1.0)
+    assert bsr_mod.calculate_accuracy_metrics([(4, 0.0)], 0, 50) == (0.0, 0.0, 0.0)
