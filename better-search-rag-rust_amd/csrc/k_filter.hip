@@ -527,7 +527,9 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     // wait for the tile's scale load is then not a full drain).  Drained before exit.
     constexpr bool kSteady = (VAR & 64) != 0 && kPr >= 2;
     constexpr bool kNoDMA = kV == 1 || kV == 6, kNoEpi = kV == 5 || kV == 6, kB2 = kPr >= 2;
-    constexpr int kS = kP == 3 ? 10 : kQsSlots, kA = kP == 3 ? 7 : kQsAhead;
+    // VAR + 128 (P = 2, tooling): a 9-slot ring with 7 slices ahead (one more DMA in flight)
+    constexpr bool kDeep = (VAR & 128) != 0 && kP == 2;
+    constexpr int kS = kP == 3 ? 10 : (kDeep ? 9 : kQsSlots), kA = kP == 3 ? 7 : (kDeep ? 7 : kQsAhead);
     static_assert(!kB2 || (kS >= kA + kP && kA >= kP + 2), "ring: slot reuse and landing margins");
     // NB query blocks of 32 per wave: NB = 2 -> 4 waves x 64 queries (one wave per SIMD);
     // NB = 1 -> 8 waves x 32 queries (two per SIMD, 96 query registers each)
