@@ -749,7 +749,8 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                 for (int n = 0; n < NB; ++n) asm volatile("" ::"v"(acc[m][n][0]));
             continue;
         }
-        // ---- epilogue
+        // ---- epilogue (VAR + 256, tooling: at raised wave priority)
+        if constexpr ((VAR & 256) != 0) __builtin_amdgcn_s_setprio(2);
         uint64_t te = 0;
         if (STAMP) te = stamp();
         bool stored = false;
@@ -818,6 +819,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
         }
         // global stores / atomics count in vmcnt: drain them so the counted waits stay exact
         if (stored) wait_vm0();
+        if constexpr ((VAR & 256) != 0) __builtin_amdgcn_s_setprio(0);
         if (STAMP) c_epi += stamp() - te;
     }
     if (kSteady) wait_vm0();  // the stream's trailing DMAs land before the workgroup ends

@@ -77,6 +77,8 @@ int main(int argc, char** argv) {
         {"S2 tau=inf", k_filter_qs8<true, 12, false, 72>, true, 1e9f, {}, {}, 512},
         {"S2 tau=0.125", k_filter_qs8<true, 12, false, 72>, true, 0.125f, {}, {}, 512},
         {"S2 no-epi", k_filter_qs8<true, 12, false, 77>, true, 1e9f, {}, {}, 512},
+        {"P2 tau=inf", k_filter_qs8<true, 12, false, 328>, true, 1e9f, {}, {}, 512},
+        {"P2 tau=0.125", k_filter_qs8<true, 12, false, 328>, true, 0.125f, {}, {}, 512},
         {"D2 tau=inf", k_filter_qs8<true, 12, false, 200>, true, 1e9f, {}, {}, 512},
         {"D2 tau=0.125", k_filter_qs8<true, 12, false, 200>, true, 0.125f, {}, {}, 512},
         {"B3 tau=inf", k_filter_qs8<true, 12, false, 16>, true, 1e9f, {}, {}, 512},
