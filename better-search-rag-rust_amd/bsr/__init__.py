@@ -12,7 +12,11 @@ reference (paths relative to nichmorgan/better-search-rag-rust):
 ``compute_local_top_k``                src/mpi_helpers/metrics.rs:16-53
 ``gather_top_k_results``               src/mpi_helpers/metrics.rs:56-138
 ``compute_global_top_k``               src/mpi_helpers/metrics.rs:141-171
+``gather_global_top_k``                src/mpi_helpers/metrics.rs:56-171 (a-4 + a-5)
 ``parallel_top_k_similarity_search``   src/mpi_helpers/metrics.rs:174-206
+``Comm`` (RCCL / host transport)       the MPI world; ``Comm.broadcast``: src/main.rs:123-125
+``run_search_stage``                   src/main.rs:109-163
+``similarity_search_report``           src/mpi_helpers/benchmark.rs:131-413
 ``calculate_accuracy_metrics``         src/mpi_helpers/metrics.rs:217-249
 ``PolarsVectorstore`` (lib/libbsr_vstore.so, include/bsr_vstore.h)
                                        src/vectorstore/polars.rs:7-247
@@ -81,6 +85,9 @@ class Profile(ctypes.Structure):
 
 _lib = None
 _P = ctypes.c_void_p
+# int (*)(const void* send, void* recv, uint64_t bytes, void* user)  (include/bsr.h)
+_HOST_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                   ctypes.c_void_p)
 
 
 def lib() -> ctypes.CDLL:
@@ -114,6 +121,10 @@ def lib() -> ctypes.CDLL:
         "bsr_comm_destroy": (None, [_P]),
         "bsr_comm_rank": (ctypes.c_int, [_P, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "bsr_gather_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
+        "bsr_comm_init_host": (ctypes.c_int, [i32, i32, _HOST_ALLGATHER, _P, ctypes.POINTER(_P)]),
+        "bsr_gather_global_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
+        "bsr_broadcast": (ctypes.c_int, [_P, _P, u64, i32]),
+        "bsr_allgather_bytes": (ctypes.c_int, [_P, _P, _P, u64]),
         "bsr_parallel_top_k_similarity_search": (ctypes.c_int, [_P, _P, _P, u32, u32, _P, _P, _P]),
         "bsr_index_last_stats": (ctypes.c_int, [_P, ctypes.POINTER(SearchStats)]),
         "bsr_index_profile": (ctypes.c_int, [_P, ctypes.POINTER(Profile), ctypes.c_int]),
@@ -317,7 +328,12 @@ class Index:
 
 # ---- communicator -----------------------------------------------------------------------
 class Comm:
-    """RCCL communicator over the ranks (one process per GPU) -- replaces the MPI world."""
+    """The rank group of the exchange step -- replaces the MPI world.
+
+    ``Comm(unique_id, rank, size, device)``: RCCL over xGMI, one GPU per rank.
+    ``Comm.host(group)``: the same gather + merge code over a host transport, here a
+    torch.distributed process group (gloo on CPU, or any backend): the library calls back
+    into Python for each all-gather of packed host bytes."""
 
     def __init__(self, unique_id: bytes, rank: int, size: int, device: int = -1):
         h = _P()
@@ -326,12 +342,58 @@ class Comm:
         self._h = h
         self.rank = rank
         self.size = size
+        self.transport = "rccl"
+
+    @classmethod
+    def host(cls, group=None) -> "Comm":
+        import torch
+        import torch.distributed as dist
+
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+
+        def allgather(send, recv, nbytes, _user):
+            try:
+                n = int(nbytes)
+                src = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(send)) if n else np.zeros(0, np.uint8)
+                t = torch.from_numpy(src.copy())
+                parts = [torch.empty(n, dtype=torch.uint8) for _ in range(size)]
+                dist.all_gather(parts, t, group=group)
+                dst = np.ctypeslib.as_array((ctypes.c_uint8 * (n * size)).from_address(recv)) if n else None
+                for r, p in enumerate(parts):
+                    if n:
+                        dst[r * n:(r + 1) * n] = p.numpy()
+                return 0
+            except Exception:  # the library reports a transport failure
+                return 1
+
+        self = cls.__new__(cls)
+        self._cb = _HOST_ALLGATHER(allgather)  # kept alive as long as the comm
+        h = _P()
+        _check(lib().bsr_comm_init_host(rank, size, self._cb, None, ctypes.byref(h)))
+        self._h = h
+        self.rank = rank
+        self.size = size
+        self.transport = "host"
+        return self
 
     @staticmethod
     def unique_id() -> bytes:
         buf = (ctypes.c_uint8 * 128)()
         _check(lib().bsr_comm_unique_id(buf))
         return bytes(buf)
+
+    def broadcast(self, array, root: int = 0):
+        """src/main.rs:123-125 process_at_rank(root).broadcast_into(array) (in place)."""
+        _check(lib().bsr_broadcast(self._h, _ptr(array), int(array.nbytes if isinstance(array, np.ndarray)
+                                                              else array.numel() * array.element_size()), root))
+        return array
+
+    def allgather_bytes(self, data: bytes) -> List[bytes]:
+        n = len(data)
+        src = np.frombuffer(data, np.uint8).copy() if n else np.zeros(1, np.uint8)
+        dst = np.empty(max(n * self.size, 1), np.uint8)
+        _check(lib().bsr_allgather_bytes(self._h, _ptr(src), _ptr(dst), n))
+        return [dst[r * n:(r + 1) * n].tobytes() for r in range(self.size)]
 
     def close(self):
         if getattr(self, "_h", None):
@@ -343,6 +405,22 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def _as_comm(world) -> Optional[Comm]:
+    """A Comm for `world`: a Comm as is, None (one rank) as None, a torch.distributed
+    group (or the default group, passed as a group object) as a cached host-transport Comm."""
+    if world is None or isinstance(world, Comm):
+        return world
+    key = id(world)
+    c = _HOST_COMMS.get(key)
+    if c is None:
+        c = Comm.host(world)
+        _HOST_COMMS[key] = c
+    return c
+
+
+_HOST_COMMS: dict = {}
 
 
 # ---- a-2 ... a-6 (reference-shaped, single query) -------------------------------------
@@ -386,47 +464,80 @@ def merge_top_k_lists(idx, dist, count, top_k: int):
 
 
 def gather_top_k_results(world, rank: int, local_top_k: List[Tuple[int, float]]):
-    """src/mpi_helpers/metrics.rs:56-138: rank-order concatenation at the root.
-
-    `world` is a torch.distributed process group (any backend, e.g. gloo on CPU) or None
-    for a single rank.  Non-root ranks get empty lists, like the reference."""
+    """src/mpi_helpers/metrics.rs:56-138: rank-order concatenation at the root, through the
+    C ABI's exchange (bsr_gather_top_k) over `world` (a Comm, a torch.distributed group or
+    None for one rank).  Non-root ranks get empty lists, like the reference."""
     local_idx = [int(i) for i, _ in local_top_k]
     local_dist = [float(d) for _, d in local_top_k]
-    if world is None:
+    comm = _as_comm(world)
+    if comm is None:
         return local_idx, local_dist
-    import torch.distributed as dist
-
-    gathered = [None] * dist.get_world_size(world)
-    dist.all_gather_object(gathered, (local_idx, local_dist), group=world)
+    # every rank sends a fixed-size slot: the largest local count (all-gathered first, as
+    # the reference's all_gather_into of the counts, :67-68)
+    counts = np.frombuffer(b"".join(comm.allgather_bytes(np.uint32(len(local_idx)).tobytes())), np.uint32)
+    kk = max(int(counts.max()), 1)
+    li = np.zeros((1, kk), np.uint64)
+    ld = np.zeros((1, kk), np.float32)
+    li[0, :len(local_idx)] = local_idx
+    ld[0, :len(local_dist)] = local_dist
+    lc = np.array([len(local_idx)], np.uint32)
+    P = comm.size
+    ri = np.zeros((P, 1, kk), np.uint64)
+    rd = np.zeros((P, 1, kk), np.float32)
+    rc = np.zeros((P, 1), np.uint32)
+    _check(lib().bsr_gather_top_k(comm._h, _ptr(li), _ptr(ld), _ptr(lc), 1, kk, _ptr(ri), _ptr(rd), _ptr(rc)))
     if rank != ROOT:
         return [], []
     gi, gd = [], []
-    for part_idx, part_dist in gathered:  # rank order
-        gi.extend(part_idx)
-        gd.extend(part_dist)
+    for r in range(P):  # rank order
+        c = int(rc[r, 0])
+        gi.extend(int(x) for x in ri[r, 0, :c])
+        gd.extend(float(x) for x in rd[r, 0, :c])
     return gi, gd
+
+
+def gather_global_top_k(world, local_idx, local_dist, local_count, top_k: int):
+    """a-4 + a-5 composed (the exchange step of parallel_top_k_similarity_search,
+    src/mpi_helpers/metrics.rs:194-202) for a batch: local lists [Q, top_k] (+ counts [Q]) of
+    this rank, or all None for an empty contribution.  Root: (idx, dist, count) of the
+    global top-k; other ranks: None."""
+    comm = _as_comm(world)
+    if local_idx is None:
+        q = None
+    else:
+        local_idx = np.ascontiguousarray(local_idx, np.uint64)
+        local_dist = np.ascontiguousarray(local_dist, np.float32)
+        local_count = np.ascontiguousarray(local_count, np.uint32)
+        q = local_idx.shape[0]
+    nq = q if q is not None else 0
+    # every rank must agree on the batch size: take it from the ranks that have lists
+    nq = int(max(np.frombuffer(b"".join(comm.allgather_bytes(np.uint32(nq).tobytes())), np.uint32)))
+    oi = np.empty((nq, top_k), np.uint64)
+    od = np.empty((nq, top_k), np.float32)
+    oc = np.empty(nq, np.uint32)
+    _check(lib().bsr_gather_global_top_k(comm._h, _ptr(local_idx), _ptr(local_dist), _ptr(local_count), nq,
+                                         top_k, _ptr(oi), _ptr(od), _ptr(oc)))
+    if comm.rank != ROOT:
+        return None
+    return oi, od, oc
 
 
 def parallel_top_k_similarity_search(world, rank: int, size: int, index: Index, top_k: int,
                                      target_vector) -> Optional[List[Tuple[int, float]]]:
-    """src/mpi_helpers/metrics.rs:174-206.  With a :class:`Comm` the whole step runs in the
-    native library (RCCL all-gather + host merge); with a torch.distributed group (or None)
-    the gather goes through torch.distributed and the merge through the C ABI."""
+    """src/mpi_helpers/metrics.rs:174-206, one query: the local search on this rank's shard
+    (GPU), the exchange over `world` (a Comm -- RCCL or host transport --, a
+    torch.distributed group, or None for one rank) and the root's merge, all inside the
+    library (bsr_parallel_top_k_similarity_search).  Root: the global top-k; others: None."""
     q = np.asarray(target_vector, np.float32).reshape(1, -1)
-    if isinstance(world, Comm) or world is None:
-        oi = np.empty((1, top_k), np.uint64)
-        od = np.empty((1, top_k), np.float32)
-        oc = np.empty(1, np.uint32)
-        _check(lib().bsr_parallel_top_k_similarity_search(world._h if world else None, index._h, _ptr(q),
-                                                          1, top_k, _ptr(oi), _ptr(od), _ptr(oc)))
-        if rank != ROOT:
-            return None
-        return [(int(oi[0, i]), float(od[0, i])) for i in range(int(oc[0]))]
-    local = compute_local_top_k(index, rank, size, top_k, q[0])
-    gi, gd = gather_top_k_results(world, rank, local)
+    comm = _as_comm(world)
+    oi = np.empty((1, top_k), np.uint64)
+    od = np.empty((1, top_k), np.float32)
+    oc = np.empty(1, np.uint32)
+    _check(lib().bsr_parallel_top_k_similarity_search(comm._h if comm else None, index._h, _ptr(q), 1, top_k,
+                                                      _ptr(oi), _ptr(od), _ptr(oc)))
     if rank != ROOT:
         return None
-    return compute_global_top_k(gi, gd, top_k)
+    return [(int(oi[0, i]), float(od[0, i])) for i in range(int(oc[0]))]
 
 
 def calculate_accuracy_metrics(top_k_results, query_idx: int, top_k: int):
@@ -457,21 +568,52 @@ def _rust_f32(x) -> str:
     return np.format_float_positional(np.float32(x), unique=True, trim="-")
 
 
+def similarity_search_report(world, rank: int, seconds: float) -> str:
+    """The "similarity_search" entry of the reference's performance report
+    (src/mpi_helpers/benchmark.rs:131-293 gathers every rank's timing to the root;
+    :296-413 prints min (first rank attaining it), max (last rank attaining it, as Rust's
+    max_by) and the average, {:.4} seconds).  Root: the report text; other ranks: ""."""
+    comm = _as_comm(world)
+    if comm is None:
+        secs = [float(seconds)]
+    else:
+        parts = comm.allgather_bytes(np.float64(seconds).tobytes())
+        secs = [float(np.frombuffer(p, np.float64)[0]) for p in parts]
+    if rank != ROOT:
+        return ""
+    mn, mx = min(secs), max(secs)
+    min_rank = secs.index(mn)
+    max_rank = len(secs) - 1 - secs[::-1].index(mx)
+    return ("==== PARALLEL PERFORMANCE REPORT ====\n\n"
+            "Operation: similarity_search\n"
+            f"  Min time: {mn:.4f} sec (Rank {min_rank})\n"
+            f"  Max time: {mx:.4f} sec (Rank {max_rank})\n"
+            f"  Avg time: {sum(secs) / len(secs):.4f} sec\n")
+
+
 def run_search_stage(world, rank: int, size: int, index: "Index", target_vector=None, top_k: int = 50,
-                     query_idx: int = 0, out=None):
-    """The driver's search stage (src/main.rs:109-163): query = row `query_idx` of rank 0's
-    store (broadcast by the caller as `target_vector`, or read from the index), the parallel
-    top-k search timed as "similarity_search", then on the root the result list and the
-    accuracy metrics printed in the reference's format.  Returns (results, metrics,
-    seconds) on the root, (None, None, seconds) elsewhere."""
+                     query_idx: int = 0, out=None, report: bool = True):
+    """The driver's search stage (src/main.rs:109-163).  The "similarity_search" timer starts
+    first (:114); unless the caller passes `target_vector`, the root reads row `query_idx` of
+    its own store (rank 0's shard starts at global row 0, :117-121) and broadcasts it to every
+    rank (:123-125); then the parallel top-k search (:130-131).  On the root the result list
+    and the accuracy metrics are printed in the reference's format (:141-163), followed by
+    the report's similarity_search entry.  Returns (results, metrics, seconds) on the root,
+    (None, None, seconds) elsewhere.  Collective: every rank calls it."""
     import sys as _sys
     import time as _time
     w = (out or _sys.stdout).write
-    if target_vector is None:
-        target_vector = index.get(query_idx)
+    comm = _as_comm(world)
     t0 = _time.perf_counter()
-    res = parallel_top_k_similarity_search(world, rank, size, index, top_k, target_vector)
+    if target_vector is None:
+        target_vector = np.zeros(index.dim, np.float32)
+        if rank == ROOT:
+            target_vector = np.ascontiguousarray(index.get(query_idx), np.float32)
+        if comm is not None:
+            comm.broadcast(target_vector, ROOT)
+    res = parallel_top_k_similarity_search(comm, rank, size, index, top_k, target_vector)
     secs = _time.perf_counter() - t0
+    rep = similarity_search_report(comm, rank, secs) if report else ""
     if rank != ROOT:
         return None, None, secs
     if res is None:
@@ -483,6 +625,8 @@ def run_search_stage(world, rank: int, size: int, index: "Index", target_vector=
     w(f"  Mean Reciprocal Rank (MRR): {mrr:.4f}\n")
     w(f"  Recall@{top_k}: {recall:.4f}\n")
     w(f"  Top-k Overlap: {overlap:.4f}\n")
+    if rep:
+        w(rep)
     return res, (mrr, recall, overlap), secs
 
 

@@ -10,6 +10,7 @@
 
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "merge.hpp"
 
 namespace bsr {
 const char* last_error_cstr();
@@ -37,15 +38,36 @@ int bsr_copy_out_impl(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx,
         return set_error(BSR_E_INVALID, "internal error (exception)");         \
     }
 
+// The rank group of the exchange step: RCCL over xGMI (one GPU per rank), or a host
+// transport given by the caller (bsr_comm_init_host: e.g. gloo/MPI stand-ins on CPU).
 struct bsr_comm {
     ncclComm_t comm = nullptr;
-    int32_t rank = 0, size = 1, device = 0;
+    int32_t rank = 0, size = 1, device = -1;
     hipStream_t stream = nullptr;
+    bsr_host_allgather_fn host_fn = nullptr;  // non-null: host transport
+    void* host_user = nullptr;
     DevBuf send_idx, send_dist, send_cnt, recv_idx, recv_dist, recv_cnt;
-    std::vector<uint64_t> h_idx;
+    std::vector<uint64_t> h_idx;   // root: gathered [size][nq][k]
     std::vector<float> h_dist;
-    std::vector<uint32_t> h_cnt;
+    std::vector<uint32_t> h_cnt;   // root: [size][nq]
+    std::vector<uint8_t> h_send, h_recv;  // host transport packing
+    std::vector<uint64_t> m_idx;   // root merge output staging (device outputs)
+    std::vector<float> m_dist;
+    std::vector<uint32_t> m_cnt;
 };
+
+// Copy to a caller buffer that may be host or device memory.
+#define BSR_HIP_OR_HOST_COPY(dst, src, bytes)                                            \
+    do {                                                                                 \
+        if (is_device_ptr(dst)) BSR_HIP(hipMemcpy((dst), (src), (bytes), hipMemcpyHostToDevice)); \
+        else memcpy((dst), (src), (bytes));                                              \
+    } while (0)
+
+#define BSR_HIP_OR_HOST_COPY_FROM(dst, src, bytes)                                       \
+    do {                                                                                 \
+        if (is_device_ptr(src)) BSR_HIP(hipMemcpy((dst), (src), (bytes), hipMemcpyDeviceToHost)); \
+        else memcpy((dst), (src), (bytes));                                              \
+    } while (0)
 
 #define BSR_NCCL(call)                                                                          \
     do {                                                                                        \
@@ -53,68 +75,6 @@ struct bsr_comm {
         if (r_ != ncclSuccess)                                                                  \
             return set_error(BSR_E_RCCL, "%s failed: %s", #call, ncclGetErrorString(r_));       \
     } while (0)
-
-// ---------------------------------------------------------------------------------------
-// host merge
-// ---------------------------------------------------------------------------------------
-namespace {
-
-struct Entry {
-    uint64_t idx;
-    float dist;
-};
-
-// src/mpi_helpers/metrics.rs:141-171 literally: concatenate (in list order), stable sort by
-// distance, dedupe by index, keep top_k.
-uint32_t global_top_k_one(const Entry* in, size_t n, uint32_t k, uint64_t* out_idx, float* out_dist,
-                          std::vector<Entry>& scratch, bool* nan) {
-    scratch.assign(in, in + n);
-    for (const Entry& e : scratch)
-        if (e.dist != e.dist) { *nan = true; return 0; }
-    std::stable_sort(scratch.begin(), scratch.end(), [](const Entry& a, const Entry& b) { return a.dist < b.dist; });
-    uint32_t out = 0;
-    for (const Entry& e : scratch) {
-        if (out >= k) break;
-        bool seen = false;
-        for (uint32_t j = 0; j < out; ++j)
-            if (out_idx[j] == e.idx) { seen = true; break; }
-        if (seen) continue;
-        out_idx[out] = e.idx;
-        out_dist[out] = e.dist;
-        ++out;
-    }
-    return out;
-}
-
-// Same result for per-rank lists already in (distance, index) order over disjoint,
-// rank-ordered index blocks (what bsr_local_top_k returns): a P-way merge.
-uint32_t merge_sorted_lists(const uint64_t* idx, const float* dist, const uint32_t* cnt, uint32_t n_lists,
-                            uint32_t n_queries, uint32_t k_in, uint32_t q, uint32_t k, uint64_t* out_idx,
-                            float* out_dist) {
-    uint32_t pos[64] = {0};
-    uint32_t out = 0;
-    while (out < k) {
-        int best = -1;
-        float bd = 0.0f;
-        uint64_t bi = 0;
-        for (uint32_t l = 0; l < n_lists; ++l) {
-            const size_t base = ((size_t)l * n_queries + q) * k_in;
-            if (pos[l] >= cnt[(size_t)l * n_queries + q]) continue;
-            const float d = dist[base + pos[l]];
-            const uint64_t i = idx[base + pos[l]];
-            if (best < 0 || d < bd || (d == bd && i < bi)) { best = (int)l; bd = d; bi = i; }
-        }
-        if (best < 0) break;
-        ++pos[best];
-        if (out && out_idx[out - 1] == bi) continue;  // dedupe (a no-op for disjoint blocks)
-        out_idx[out] = bi;
-        out_dist[out] = bd;
-        ++out;
-    }
-    return out;
-}
-
-}  // namespace
 
 // ---------------------------------------------------------------------------------------
 // C ABI
@@ -229,24 +189,8 @@ static int global_top_k_impl(const uint64_t* idx, const float* dist, const uint3
     if (!count || !out_idx || !out_dist || !out_count || (n_lists && k_in && (!idx || !dist)))
         return set_error(BSR_E_INVALID, "null argument");
     if (k == 0) return set_error(BSR_E_INVALID, "k must be >= 1");
-    std::vector<Entry> concat, scratch;
-    for (uint32_t q = 0; q < n_queries; ++q) {
-        concat.clear();
-        for (uint32_t l = 0; l < n_lists; ++l) {
-            const uint32_t c = std::min(count[(size_t)l * n_queries + q], k_in);
-            const size_t base = ((size_t)l * n_queries + q) * k_in;
-            for (uint32_t i = 0; i < c; ++i) concat.push_back({idx[base + i], dist[base + i]});
-        }
-        bool nan = false;
-        out_count[q] = global_top_k_one(concat.data(), concat.size(), k, out_idx + (size_t)q * k,
-                                        out_dist + (size_t)q * k, scratch, &nan);
-        if (nan) return set_error(BSR_E_NONFINITE, "NaN distance in query %u (the reference panics)", q);
-        for (uint32_t i = out_count[q]; i < k; ++i) {
-            out_idx[(size_t)q * k + i] = ~0ull;
-            out_dist[(size_t)q * k + i] = __builtin_inff();
-        }
-    }
-    return BSR_OK;
+    return merge_top_k_lists(ListsView{idx, dist, count, n_lists, n_queries, k_in}, n_queries, k, out_idx, out_dist,
+                             out_count);
 }
 
 int bsr_global_top_k(const uint64_t* idx, const float* dist, const uint32_t* count, uint32_t n_lists,
@@ -294,12 +238,29 @@ int bsr_comm_init(const uint8_t id[BSR_UNIQUE_ID_BYTES], int32_t rank, int32_t s
     BSR_GUARD(comm_init_impl(id, rank, size, device, out));
 }
 
+static int comm_init_host_impl(int32_t rank, int32_t size, bsr_host_allgather_fn fn, void* user, bsr_comm** out) {
+    if (!out || !fn || size < 1 || rank < 0 || rank >= size) return set_error(BSR_E_INVALID, "bad argument");
+    bsr_comm* c = new bsr_comm();
+    c->rank = rank;
+    c->size = size;
+    c->host_fn = fn;
+    c->host_user = user;
+    *out = c;
+    return BSR_OK;
+}
+
+int bsr_comm_init_host(int32_t rank, int32_t size, bsr_host_allgather_fn fn, void* user, bsr_comm** out) {
+    BSR_GUARD(comm_init_host_impl(rank, size, fn, user, out));
+}
+
 void bsr_comm_destroy(bsr_comm* c) {
     if (!c) return;
     try {
-        (void)hipSetDevice(c->device);
-        if (c->stream) { (void)hipStreamSynchronize(c->stream); (void)hipStreamDestroy(c->stream); }
-        if (c->comm) ncclCommDestroy(c->comm);
+        if (c->comm) {
+            (void)hipSetDevice(c->device);
+            if (c->stream) { (void)hipStreamSynchronize(c->stream); (void)hipStreamDestroy(c->stream); }
+            ncclCommDestroy(c->comm);
+        }
         delete c;
     } catch (...) {}
 }
@@ -311,18 +272,111 @@ int bsr_comm_rank(const bsr_comm* c, int32_t* rank, int32_t* size) {
     return BSR_OK;
 }
 
-// All-gather the [nq][k] partial lists of every rank (device buffers) on `stream`.
-static int allgather_lists(bsr_comm* c, const uint64_t* d_idx, const float* d_dist, const uint32_t* d_cnt,
-                           uint32_t nq, uint32_t k, hipStream_t stream) {
-    const size_t nk = (size_t)nq * k;
-    BSR_TRY(c->recv_idx.ensure(nk * c->size * sizeof(uint64_t)));
-    BSR_TRY(c->recv_dist.ensure(nk * c->size * sizeof(float)));
-    BSR_TRY(c->recv_cnt.ensure((size_t)nq * c->size * sizeof(uint32_t)));
+// ---------------------------------------------------------------------------------------
+// The exchange step (gather_top_k_results, src/mpi_helpers/metrics.rs:56-138): every rank's
+// [nq][k] partial lists (+ counts) reach the root in rank order, as c->h_idx / h_dist /
+// h_cnt laid out [rank][nq][k].  RCCL: one group of three all-gathers on `stream` (lists on
+// the device, or staged there); host transport: one packed all-gather through the caller's
+// function.  `empty`: this rank contributes empty lists (its local search failed:
+// :185-191 sends an empty vector and the gather still completes).
+// ---------------------------------------------------------------------------------------
+static int exchange_lists(bsr_comm* c, const uint64_t* idx, const float* dist, const uint32_t* cnt, bool empty,
+                          uint32_t nq, uint32_t k, hipStream_t stream) {
+    const size_t nk = (size_t)nq * k, P = (size_t)c->size;
+    const bool root = c->rank == 0;
+    if (c->host_fn) {
+        // message per rank: counts [nq] u32 | dists [nq][k] f32 | indices [nq][k] u64
+        const size_t o_dist = (size_t)nq * 4, o_idx = o_dist + nk * 4, bytes = o_idx + nk * 8;
+        c->h_send.assign(bytes, 0);
+        c->h_recv.resize(bytes * P);
+        if (!empty) {
+            const bool dev = is_device_ptr(idx) || is_device_ptr(dist) || is_device_ptr(cnt);
+            if (dev) {
+                BSR_HIP(hipMemcpy(c->h_send.data(), cnt, (size_t)nq * 4, hipMemcpyDefault));
+                BSR_HIP(hipMemcpy(c->h_send.data() + o_dist, dist, nk * 4, hipMemcpyDefault));
+                BSR_HIP(hipMemcpy(c->h_send.data() + o_idx, idx, nk * 8, hipMemcpyDefault));
+            } else {
+                memcpy(c->h_send.data(), cnt, (size_t)nq * 4);
+                memcpy(c->h_send.data() + o_dist, dist, nk * 4);
+                memcpy(c->h_send.data() + o_idx, idx, nk * 8);
+            }
+        }
+        if (c->host_fn(c->h_send.data(), c->h_recv.data(), bytes, c->host_user) != 0)
+            return set_error(BSR_E_RCCL, "host all-gather callback failed");
+        if (root) {
+            c->h_cnt.resize((size_t)nq * P);
+            c->h_dist.resize(nk * P);
+            c->h_idx.resize(nk * P);
+            for (size_t r = 0; r < P; ++r) {
+                const uint8_t* m = c->h_recv.data() + r * bytes;
+                memcpy(c->h_cnt.data() + r * nq, m, (size_t)nq * 4);
+                memcpy(c->h_dist.data() + r * nk, m + o_dist, nk * 4);
+                memcpy(c->h_idx.data() + r * nk, m + o_idx, nk * 8);
+            }
+        }
+        return BSR_OK;
+    }
+    BSR_HIP(hipSetDevice(c->device));
+    const uint64_t* s_idx = idx;
+    const float* s_dist = dist;
+    const uint32_t* s_cnt = cnt;
+    if (empty || !is_device_ptr(idx) || !is_device_ptr(dist) || !is_device_ptr(cnt)) {
+        BSR_TRY(c->send_idx.ensure(nk * sizeof(uint64_t)));
+        BSR_TRY(c->send_dist.ensure(nk * sizeof(float)));
+        BSR_TRY(c->send_cnt.ensure((size_t)nq * sizeof(uint32_t)));
+        if (empty) {
+            BSR_HIP(hipMemsetAsync(c->send_cnt.p, 0, (size_t)nq * sizeof(uint32_t), stream));
+        } else {
+            BSR_HIP(hipMemcpyAsync(c->send_idx.p, idx, nk * sizeof(uint64_t), hipMemcpyDefault, stream));
+            BSR_HIP(hipMemcpyAsync(c->send_dist.p, dist, nk * sizeof(float), hipMemcpyDefault, stream));
+            BSR_HIP(hipMemcpyAsync(c->send_cnt.p, cnt, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, stream));
+        }
+        s_idx = c->send_idx.as<uint64_t>();
+        s_dist = c->send_dist.as<float>();
+        s_cnt = c->send_cnt.as<uint32_t>();
+    }
+    BSR_TRY(c->recv_idx.ensure(nk * P * sizeof(uint64_t)));
+    BSR_TRY(c->recv_dist.ensure(nk * P * sizeof(float)));
+    BSR_TRY(c->recv_cnt.ensure((size_t)nq * P * sizeof(uint32_t)));
     BSR_NCCL(ncclGroupStart());
-    BSR_NCCL(ncclAllGather(d_idx, c->recv_idx.p, nk * sizeof(uint64_t), ncclUint8, c->comm, stream));
-    BSR_NCCL(ncclAllGather(d_dist, c->recv_dist.p, nk * sizeof(float), ncclUint8, c->comm, stream));
-    BSR_NCCL(ncclAllGather(d_cnt, c->recv_cnt.p, (size_t)nq * sizeof(uint32_t), ncclUint8, c->comm, stream));
+    BSR_NCCL(ncclAllGather(s_idx, c->recv_idx.p, nk * sizeof(uint64_t), ncclUint8, c->comm, stream));
+    BSR_NCCL(ncclAllGather(s_dist, c->recv_dist.p, nk * sizeof(float), ncclUint8, c->comm, stream));
+    BSR_NCCL(ncclAllGather(s_cnt, c->recv_cnt.p, (size_t)nq * sizeof(uint32_t), ncclUint8, c->comm, stream));
     BSR_NCCL(ncclGroupEnd());
+    if (root) {
+        c->h_idx.resize(nk * P);
+        c->h_dist.resize(nk * P);
+        c->h_cnt.resize((size_t)nq * P);
+        BSR_HIP(hipMemcpyAsync(c->h_idx.data(), c->recv_idx.p, nk * P * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        BSR_HIP(hipMemcpyAsync(c->h_dist.data(), c->recv_dist.p, nk * P * sizeof(float), hipMemcpyDeviceToHost, stream));
+        BSR_HIP(hipMemcpyAsync(c->h_cnt.data(), c->recv_cnt.p, (size_t)nq * P * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               stream));
+    }
+    BSR_HIP(hipStreamSynchronize(stream));
+    return BSR_OK;
+}
+
+// Non-root outputs: the reference returns None; counts read 0 (host or device memory).
+static int clear_counts(uint32_t* out_count, uint32_t nq) {
+    if (!out_count || !nq) return BSR_OK;
+    if (is_device_ptr(out_count)) BSR_HIP(hipMemset(out_count, 0, (size_t)nq * sizeof(uint32_t)));
+    else memset(out_count, 0, (size_t)nq * sizeof(uint32_t));
+    return BSR_OK;
+}
+
+// The root's merge (compute_global_top_k, :200-202) of the gathered lists into out_*.
+static int root_merge(bsr_comm* c, uint32_t nq, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
+    const ListsView v{c->h_idx.data(), c->h_dist.data(), c->h_cnt.data(), (uint32_t)c->size, nq, k};
+    const bool dev = is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count);
+    if (!dev) return merge_top_k_lists(v, nq, k, out_idx, out_dist, out_count);
+    const size_t nk = (size_t)nq * k;
+    c->m_idx.resize(nk);
+    c->m_dist.resize(nk);
+    c->m_cnt.resize(nq);
+    BSR_TRY(merge_top_k_lists(v, nq, k, c->m_idx.data(), c->m_dist.data(), c->m_cnt.data()));
+    BSR_HIP(hipMemcpy(out_idx, c->m_idx.data(), nk * sizeof(uint64_t), hipMemcpyHostToDevice));
+    BSR_HIP(hipMemcpy(out_dist, c->m_dist.data(), nk * sizeof(float), hipMemcpyHostToDevice));
+    BSR_HIP(hipMemcpy(out_count, c->m_cnt.data(), (size_t)nq * sizeof(uint32_t), hipMemcpyHostToDevice));
     return BSR_OK;
 }
 
@@ -332,23 +386,13 @@ static int gather_impl(bsr_comm* c, const uint64_t* local_idx, const float* loca
     if (!nq) return BSR_OK;
     if (!local_idx || !local_dist || !local_count || k == 0) return set_error(BSR_E_INVALID, "bad argument");
     if (c->rank == 0 && (!root_idx || !root_dist || !root_count)) return set_error(BSR_E_INVALID, "null root output");
-    BSR_HIP(hipSetDevice(c->device));
-    const size_t nk = (size_t)nq * k;
-    BSR_TRY(c->send_idx.ensure(nk * sizeof(uint64_t)));
-    BSR_TRY(c->send_dist.ensure(nk * sizeof(float)));
-    BSR_TRY(c->send_cnt.ensure((size_t)nq * sizeof(uint32_t)));
-    BSR_HIP(hipMemcpyAsync(c->send_idx.p, local_idx, nk * sizeof(uint64_t), hipMemcpyDefault, c->stream));
-    BSR_HIP(hipMemcpyAsync(c->send_dist.p, local_dist, nk * sizeof(float), hipMemcpyDefault, c->stream));
-    BSR_HIP(hipMemcpyAsync(c->send_cnt.p, local_count, (size_t)nq * sizeof(uint32_t), hipMemcpyDefault, c->stream));
-    BSR_TRY(allgather_lists(c, c->send_idx.as<uint64_t>(), c->send_dist.as<float>(), c->send_cnt.as<uint32_t>(), nq,
-                            k, c->stream));
+    BSR_TRY(exchange_lists(c, local_idx, local_dist, local_count, false, nq, k, c->stream));
     if (c->rank == 0) {
-        BSR_HIP(hipMemcpyAsync(root_idx, c->recv_idx.p, nk * c->size * sizeof(uint64_t), hipMemcpyDefault, c->stream));
-        BSR_HIP(hipMemcpyAsync(root_dist, c->recv_dist.p, nk * c->size * sizeof(float), hipMemcpyDefault, c->stream));
-        BSR_HIP(hipMemcpyAsync(root_count, c->recv_cnt.p, (size_t)nq * c->size * sizeof(uint32_t), hipMemcpyDefault,
-                               c->stream));
+        const size_t nk = (size_t)nq * k * c->size;
+        BSR_HIP_OR_HOST_COPY(root_idx, c->h_idx.data(), nk * sizeof(uint64_t));
+        BSR_HIP_OR_HOST_COPY(root_dist, c->h_dist.data(), nk * sizeof(float));
+        BSR_HIP_OR_HOST_COPY(root_count, c->h_cnt.data(), (size_t)nq * c->size * sizeof(uint32_t));
     }
-    BSR_HIP(hipStreamSynchronize(c->stream));
     return BSR_OK;
 }
 
@@ -357,79 +401,134 @@ int bsr_gather_top_k(bsr_comm* c, const uint64_t* local_idx, const float* local_
     BSR_GUARD(gather_impl(c, local_idx, local_dist, local_count, n_queries, k, root_idx, root_dist, root_count));
 }
 
+static int gather_global_impl(bsr_comm* c, const uint64_t* local_idx, const float* local_dist,
+                              const uint32_t* local_count, uint32_t nq, uint32_t k, uint64_t* out_idx,
+                              float* out_dist, uint32_t* out_count) {
+    if (!c) return set_error(BSR_E_INVALID, "null communicator");
+    if (!nq) return BSR_OK;
+    if (k == 0) return set_error(BSR_E_INVALID, "k must be >= 1");
+    const bool root = c->rank == 0;
+    if (root && (!out_idx || !out_dist || !out_count)) return set_error(BSR_E_INVALID, "null root output");
+    const bool empty = !local_idx || !local_dist || !local_count;  // an empty contribution
+    BSR_TRY(exchange_lists(c, local_idx, local_dist, local_count, empty, nq, k, c->stream));
+    if (!root) return clear_counts(out_count, nq);
+    return root_merge(c, nq, k, out_idx, out_dist, out_count);
+}
+
+int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const float* local_dist,
+                            const uint32_t* local_count, uint32_t n_queries, uint32_t k, uint64_t* out_idx,
+                            float* out_dist, uint32_t* out_count) {
+    BSR_GUARD(gather_global_impl(comm, local_idx, local_dist, local_count, n_queries, k, out_idx, out_dist, out_count));
+}
+
 static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
                          uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
     if (!ix) return set_error(BSR_E_INVALID, "null index");
-    const bool single = !c || c->size == 1;
     const bool root = !c || c->rank == 0;
     if (nq && root && (!out_idx || !out_dist || !out_count)) return set_error(BSR_E_INVALID, "null output");
-    if (c && c->device != ix->device) return set_error(BSR_E_INVALID, "communicator and index on different devices");
-    // compute_local_top_k (:185-191; an error there is an error here, not an empty list)
-    BSR_TRY(ix->search_device(queries, nq, k));
-    if (!nq) return BSR_OK;
-    const size_t nk = (size_t)nq * k;
-    if (single) {
+    if (c && !c->host_fn && c->device != ix->device)
+        return set_error(BSR_E_INVALID, "communicator and index on different devices");
+    // compute_local_top_k (:185-191)
+    const int st = ix->search_device(queries, nq, k);
+    if (!c) {  // one rank, no communicator: the local lists are the result
+        BSR_TRY(st);
+        if (!nq) return BSR_OK;
         BSR_TRY(bsr_copy_out_impl(ix, nq, k, out_idx, out_dist, out_count));
         bsr_index_collect_profile_impl(ix);
         return BSR_OK;
     }
-    // gather_top_k_results (:194) as an RCCL all-gather on the index's stream, then the
-    // root's merge (:200-202).
-    BSR_TRY(allgather_lists(c, ix->d_idx, ix->d_dist, ix->d_cnt, nq, k, ix->stream));
-    if (root) {
-        c->h_idx.resize(nk * c->size);
-        c->h_dist.resize(nk * c->size);
-        c->h_cnt.resize((size_t)nq * c->size);
-        BSR_HIP(hipMemcpyAsync(c->h_idx.data(), c->recv_idx.p, nk * c->size * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                               ix->stream));
-        BSR_HIP(hipMemcpyAsync(c->h_dist.data(), c->recv_dist.p, nk * c->size * sizeof(float), hipMemcpyDeviceToHost,
-                               ix->stream));
-        BSR_HIP(hipMemcpyAsync(c->h_cnt.data(), c->recv_cnt.p, (size_t)nq * c->size * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, ix->stream));
+    if (!nq) return st;
+    if (k == 0) return st != BSR_OK ? st : set_error(BSR_E_INVALID, "k must be >= 1");
+    // A rank whose local search failed still takes part in the exchange with an empty list,
+    // as the reference does (:185-191), so no other rank blocks in the collective; it returns
+    // its own error afterwards.  The root's lists then cover the other ranks.
+    std::string local_err;
+    if (st != BSR_OK) local_err = last_error_cstr();
+    const bool ok = st == BSR_OK;
+    // gather_top_k_results (:194) on the index's stream (ordered after the search), then the
+    // root's merge (:200-202)
+    // (RCCL: the device lists; host transport: their pinned host mirror)
+    const uint64_t* li = ix->d_idx;
+    const float* ld = ix->d_dist;
+    const uint32_t* lc = ix->d_cnt;
+    if (c->host_fn) {
+        li = reinterpret_cast<const uint64_t*>(ix->h_res + ix->res_off_idx);
+        ld = reinterpret_cast<const float*>(ix->h_res + ix->res_off_dist);
+        lc = reinterpret_cast<const uint32_t*>(ix->h_res + ix->res_off_cnt);
     }
-    BSR_HIP(hipStreamSynchronize(ix->stream));
-    bsr_index_collect_profile_impl(ix);
-    if (!root) {
-        if (out_count)
-            for (uint32_t q = 0; q < nq; ++q) out_count[q] = 0;  // the reference's None
-        return BSR_OK;
-    }
-    const bool host_out = !is_device_ptr(out_idx);
-    std::vector<uint64_t> tmp_idx;
-    std::vector<float> tmp_dist;
-    std::vector<uint32_t> tmp_cnt;
-    uint64_t* oi = out_idx;
-    float* od = out_dist;
-    uint32_t* oc = out_count;
-    if (!host_out) {
-        tmp_idx.resize(nk);
-        tmp_dist.resize(nk);
-        tmp_cnt.resize(nq);
-        oi = tmp_idx.data();
-        od = tmp_dist.data();
-        oc = tmp_cnt.data();
-    }
-    if (c->size > 64) return set_error(BSR_E_INVALID, "at most 64 ranks");
-    for (uint32_t q = 0; q < nq; ++q) {
-        const uint32_t got = merge_sorted_lists(c->h_idx.data(), c->h_dist.data(), c->h_cnt.data(), (uint32_t)c->size,
-                                                nq, k, q, k, oi + (size_t)q * k, od + (size_t)q * k);
-        oc[q] = got;
-        for (uint32_t i = got; i < k; ++i) {
-            oi[(size_t)q * k + i] = ~0ull;
-            od[(size_t)q * k + i] = __builtin_inff();
-        }
-    }
-    if (!host_out) {
-        BSR_HIP(hipMemcpy(out_idx, oi, nk * sizeof(uint64_t), hipMemcpyHostToDevice));
-        BSR_HIP(hipMemcpy(out_dist, od, nk * sizeof(float), hipMemcpyHostToDevice));
-        BSR_HIP(hipMemcpy(out_count, oc, (size_t)nq * sizeof(uint32_t), hipMemcpyHostToDevice));
-    }
+    BSR_TRY(exchange_lists(c, ok ? li : nullptr, ok ? ld : nullptr, ok ? lc : nullptr, !ok, nq, k,
+                           c->host_fn ? nullptr : ix->stream));
+    if (ok) bsr_index_collect_profile_impl(ix);
+    if (root) BSR_TRY(root_merge(c, nq, k, out_idx, out_dist, out_count));
+    else BSR_TRY(clear_counts(out_count, nq));
+    if (!ok) return set_error(st, "%s", local_err.c_str());
     return BSR_OK;
 }
 
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries, uint32_t n_queries,
                                          uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
     BSR_GUARD(parallel_impl(comm, ix, queries, n_queries, k, out_idx, out_dist, out_count));
+}
+
+// ---------------------------------------------------------------------------------------
+// Small collectives of the driver (src/main.rs:123-125 broadcast_into; the timing gather of
+// src/mpi_helpers/benchmark.rs:131-293): host or device buffers, either transport.
+// ---------------------------------------------------------------------------------------
+static int allgather_bytes_impl(bsr_comm* c, const void* send, void* recv, uint64_t bytes) {
+    if (!c || (bytes && (!send || !recv))) return set_error(BSR_E_INVALID, "bad argument");
+    if (!bytes) return BSR_OK;
+    const size_t P = (size_t)c->size;
+    if (c->host_fn) {
+        std::vector<uint8_t> hs(bytes), hr(bytes * P);
+        BSR_HIP_OR_HOST_COPY_FROM(hs.data(), send, bytes);
+        if (c->host_fn(hs.data(), hr.data(), bytes, c->host_user) != 0)
+            return set_error(BSR_E_RCCL, "host all-gather callback failed");
+        BSR_HIP_OR_HOST_COPY(recv, hr.data(), bytes * P);
+        return BSR_OK;
+    }
+    BSR_HIP(hipSetDevice(c->device));
+    DevBuf ds, dr;
+    BSR_TRY(ds.ensure(bytes));
+    BSR_TRY(dr.ensure(bytes * P));
+    BSR_HIP(hipMemcpyAsync(ds.p, send, bytes, hipMemcpyDefault, c->stream));
+    BSR_NCCL(ncclAllGather(ds.p, dr.p, bytes, ncclUint8, c->comm, c->stream));
+    BSR_HIP(hipMemcpyAsync(recv, dr.p, bytes * P, hipMemcpyDefault, c->stream));
+    BSR_HIP(hipStreamSynchronize(c->stream));
+    return BSR_OK;
+}
+
+int bsr_allgather_bytes(bsr_comm* comm, const void* send, void* recv, uint64_t bytes) {
+    BSR_GUARD(allgather_bytes_impl(comm, send, recv, bytes));
+}
+
+static int broadcast_impl(bsr_comm* c, void* buf, uint64_t bytes, int32_t root) {
+    if (!c || (bytes && !buf) || root < 0 || root >= c->size) return set_error(BSR_E_INVALID, "bad argument");
+    if (!bytes) return BSR_OK;
+    if (c->host_fn) {  // a broadcast as an all-gather of which every rank keeps the root's part
+        std::vector<uint8_t> hs(bytes), hr(bytes * (size_t)c->size);
+        BSR_HIP_OR_HOST_COPY_FROM(hs.data(), buf, bytes);
+        if (c->host_fn(hs.data(), hr.data(), bytes, c->host_user) != 0)
+            return set_error(BSR_E_RCCL, "host all-gather callback failed");
+        BSR_HIP_OR_HOST_COPY(buf, hr.data() + (size_t)root * bytes, bytes);
+        return BSR_OK;
+    }
+    BSR_HIP(hipSetDevice(c->device));
+    void* d = buf;
+    DevBuf tmp;
+    const bool dev = is_device_ptr(buf);
+    if (!dev) {
+        BSR_TRY(tmp.ensure(bytes));
+        BSR_HIP(hipMemcpyAsync(tmp.p, buf, bytes, hipMemcpyHostToDevice, c->stream));
+        d = tmp.p;
+    }
+    BSR_NCCL(ncclBroadcast(d, d, bytes, ncclUint8, root, c->comm, c->stream));
+    if (!dev) BSR_HIP(hipMemcpyAsync(buf, d, bytes, hipMemcpyDeviceToHost, c->stream));
+    BSR_HIP(hipStreamSynchronize(c->stream));
+    return BSR_OK;
+}
+
+int bsr_broadcast(bsr_comm* comm, void* buf, uint64_t bytes, int32_t root) {
+    BSR_GUARD(broadcast_impl(comm, buf, bytes, root));
 }
 
 int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out) {

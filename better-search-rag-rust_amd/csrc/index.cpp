@@ -63,6 +63,14 @@ void DevBuf::release() {
 
 bool is_device_ptr(const void* p) {
     if (!p) return false;
+    // no device visible (host-only entry points on a CPU machine): every pointer is host
+    static const bool have_device = [] {
+        int n = 0;
+        const bool ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    if (!have_device) return false;
     hipPointerAttribute_t attr;
     hipError_t e = hipPointerGetAttributes(&attr, p);
     if (e != hipSuccess) {

@@ -17,9 +17,13 @@
  *   bsr_local_top_k                   src/mpi_helpers/metrics.rs:16-53 (compute_local_top_k)
  *   bsr_gather_top_k                  src/mpi_helpers/metrics.rs:56-138 (gather_top_k_results)
  *   bsr_global_top_k                  src/mpi_helpers/metrics.rs:141-171 (compute_global_top_k)
+ *   bsr_gather_global_top_k           src/mpi_helpers/metrics.rs:56-171 (a-4 + a-5: the
+ *                                     exchange and root merge of a-6, :194-202)
  *   bsr_parallel_top_k_similarity_search
  *                                     src/mpi_helpers/metrics.rs:174-206
  *                                     (parallel_top_k_similarity_search)
+ *   bsr_broadcast                     src/main.rs:123-125 (broadcast_into of the query)
+ *   bsr_allgather_bytes               src/mpi_helpers/benchmark.rs:131-293 (timing gather)
  *
  * Results are bit-identical to the reference's: indices in (distance asc, index asc)
  * order, each distance the exact f32 the reference computes (sequential f32 sums, no FMA,
@@ -154,6 +158,14 @@ int bsr_comm_init(const uint8_t id[BSR_UNIQUE_ID_BYTES], int32_t rank, int32_t s
 void bsr_comm_destroy(bsr_comm* comm);
 int bsr_comm_rank(const bsr_comm* comm, int32_t* rank, int32_t* size);
 
+/* Host transport for bsr_comm_init_host: an all-gather of `bytes` bytes from every rank
+ * into recv (size * bytes, rank order), called collectively by every rank.  Returns 0 on
+ * success.  Lets a caller run the exchange over its own transport (MPI, gloo, a test
+ * harness) with the same gather + merge code as the RCCL path. */
+typedef int (*bsr_host_allgather_fn)(const void* send, void* recv, uint64_t bytes, void* user);
+int bsr_comm_init_host(int32_t rank, int32_t size, bsr_host_allgather_fn fn, void* user,
+                       bsr_comm** out);
+
 /* ---- a-4: gather_top_k_results.  Every rank passes its [n_queries][k] local lists;
  * the root (rank 0) receives [size][n_queries][k] lists + counts in rank order
  * (host buffers, may be NULL on non-root ranks).  Collective: every rank calls it. ---- */
@@ -161,13 +173,30 @@ int bsr_gather_top_k(bsr_comm* comm, const uint64_t* local_idx, const float* loc
                      const uint32_t* local_count, uint32_t n_queries, uint32_t k,
                      uint64_t* root_idx, float* root_dist, uint32_t* root_count);
 
+/* ---- a-4 + a-5 composed (the exchange step of a-6): every rank passes its
+ * [n_queries][k] local lists (host or device; all three NULL = an empty contribution, what
+ * the reference sends after a local error, src/mpi_helpers/metrics.rs:185-191); the root
+ * gets the global top-k (rank-order concatenation, stable sort by distance, dedupe by
+ * index, :141-171) in out_*; other ranks get out_count[q] = 0.  Collective. ---------- */
+int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const float* local_dist,
+                            const uint32_t* local_count, uint32_t n_queries, uint32_t k,
+                            uint64_t* out_idx, float* out_dist, uint32_t* out_count);
+
 /* ---- a-6: parallel_top_k_similarity_search: local search on this rank's shard,
- * RCCL all-gather of the partial lists, host merge.  Root gets the global top-k in
- * out_*; other ranks get out_count[q] = 0 (the reference's None).  comm may be NULL for
- * a single-rank run. ----------------------------------------------------------------- */
+ * RCCL all-gather of the partial lists (bsr_gather_global_top_k), host merge.  Root gets
+ * the global top-k in out_*; other ranks get out_count[q] = 0 (the reference's None).
+ * comm may be NULL for a single-rank run (no exchange).  A rank whose local search fails
+ * still completes the exchange with an empty list (:185-191) and then returns its error;
+ * the root's lists cover the other ranks. --------------------------------------------- */
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries,
                                          uint32_t n_queries, uint32_t k, uint64_t* out_idx,
                                          float* out_dist, uint32_t* out_count);
+
+/* ---- driver collectives: src/main.rs:123-125 (process_at_rank(ROOT).broadcast_into of the
+ * query) and the timing gather of src/mpi_helpers/benchmark.rs:131-293.  Host or device
+ * buffers; collective over the comm (RCCL or host transport). ------------------------ */
+int bsr_broadcast(bsr_comm* comm, void* buf, uint64_t bytes, int32_t root);
+int bsr_allgather_bytes(bsr_comm* comm, const void* send, void* recv, uint64_t bytes);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out);

@@ -136,3 +136,105 @@ def test_synth_generator_replica_is_deterministic(bsr_mod):
     b = bsr_mod.synth_uniform_np(0, 14, 768, 42)[10:]
     assert np.array_equal(a, b)
     assert a.min() >= -1 and a.max() < 1 and abs(float(a.mean())) < 0.05
+
+
+def _lists_from(oracle_mod, rows, qs, P, k, offsets=None):
+    """Per-rank local lists [P, Q, k] (+ counts) of the oracle over interval_by_rank blocks;
+    `offsets` (optional) shifts each rank's indices (caller-chosen global offsets)."""
+    Q = len(qs)
+    li = np.zeros((P, Q, k), np.uint64)
+    ld = np.zeros((P, Q, k), np.float32)
+    lc = np.zeros((P, Q), np.uint32)
+    for r in range(P):
+        for q in range(Q):
+            i, d = oracle_mod.local_top_k(rows, r, P, k, qs[q])
+            if offsets is not None:
+                i = i - np.uint64(oracle_mod.interval_by_rank(r, P, len(rows))[0]) + np.uint64(offsets[r])
+            li[r, q, :len(i)] = i
+            ld[r, q, :len(d)] = d
+            lc[r, q] = len(i)
+    return li, ld, lc
+
+
+def _oracle_merge(oracle_mod, li, ld, lc, k):
+    """compute_global_top_k of the oracle over the rank-order concatenation, per query."""
+    P, Q, _ = li.shape
+    out = []
+    for q in range(Q):
+        gi = np.concatenate([li[r, q, :lc[r, q]] for r in range(P)])
+        gd = np.concatenate([ld[r, q, :lc[r, q]] for r in range(P)])
+        out.append(oracle_mod.global_top_k(gi, gd, k))
+    return out
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
+def test_merge_p_way_vs_oracle(bsr_mod, oracle_mod, P):
+    """The root merge of the parallel path (merge.cpp) vs the reference's rank-order
+    concatenation + stable sort + dedupe, at P = 2..8: cross-rank distance ties (duplicate
+    rows in different blocks, an all-equal-distance corpus slice), empty blocks (N < P)."""
+    rng = np.random.default_rng(100 + P)
+    for n in (P - 1, P + 1, 257):
+        if n < 1:
+            continue
+        rows = rng.uniform(-1, 1, (n, 24)).astype(np.float32)
+        if n > 200:
+            rows[200] = rows[3]      # tie across ranks
+            rows[150:170] = rows[10]  # a run of equal distances spanning block boundaries
+        qs = rng.uniform(-1, 1, (5, 24)).astype(np.float32)
+        qs[0] = rows[min(3, n - 1)]
+        for k in (1, 4, 16):
+            li, ld, lc = _lists_from(oracle_mod, rows, qs, P, k)
+            oi, od, oc = bsr_mod.merge_top_k_lists(li, ld, lc, k)
+            wi, wd, wc = oracle_mod.parallel_top_k(rows, qs, k, size=P)
+            assert np.array_equal(oc, wc), (n, k)
+            for q in range(len(qs)):
+                c = int(wc[q])
+                assert np.array_equal(oi[q, :c], wi[q, :c]), (n, k, q)
+                assert np.array_equal(od[q, :c].view(np.uint32), wd[q, :c].view(np.uint32))
+                assert (oi[q, c:] == np.uint64(2**64 - 1)).all() and np.isinf(od[q, c:]).all()
+
+
+def test_merge_overlapping_offsets_and_unsorted_vs_oracle(bsr_mod, oracle_mod):
+    """Overlapping blocks (every rank's offset 0: the same index from several ranks, kept
+    once, first occurrence) and lists not ordered by distance (the literal stable sort)."""
+    rng = np.random.default_rng(8)
+    rows = rng.uniform(-1, 1, (90, 16)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (4, 16)).astype(np.float32)
+    for P in (2, 5, 8):
+        li, ld, lc = _lists_from(oracle_mod, rows, qs, P, 12, offsets=[0] * P)
+        for shuffle in (False, True):
+            if shuffle:
+                for r in range(P):
+                    for q in range(4):
+                        perm = rng.permutation(int(lc[r, q]))
+                        li[r, q, :lc[r, q]] = li[r, q, perm]
+                        ld[r, q, :lc[r, q]] = ld[r, q, perm]
+            oi, od, oc = bsr_mod.merge_top_k_lists(li, ld, lc, 12)
+            for q, (wi, wd) in enumerate(_oracle_merge(oracle_mod, li, ld, lc, 12)):
+                assert int(oc[q]) == len(wi)
+                assert np.array_equal(oi[q, :len(wi)], wi) and np.array_equal(od[q, :len(wd)].view(np.uint32),
+                                                                              wd.view(np.uint32))
+                assert len(set(oi[q, :oc[q]].tolist())) == int(oc[q])  # deduped
+
+
+def test_merge_nan_is_an_error(bsr_mod):
+    li = np.zeros((2, 1, 2), np.uint64)
+    ld = np.array([[[0.1, np.nan]], [[0.2, 0.3]]], np.float32)
+    lc = np.full((2, 1), 2, np.uint32)
+    with pytest.raises(bsr_mod.BsrError) as e:
+        bsr_mod.merge_top_k_lists(li, ld, lc, 2)
+    assert e.value.status == -2
+
+
+def test_merge_large_batch_threads_vs_single(bsr_mod):
+    """The host merge splits big batches over threads: same result as query by query."""
+    rng = np.random.default_rng(4)
+    P, Q, k = 8, 3000, 100
+    ld = np.sort(rng.choice(np.linspace(0, 1, 50, dtype=np.float32), (P, Q, k)), axis=2).astype(np.float32)
+    li = (np.arange(P, dtype=np.uint64)[:, None, None] * 1000 + rng.integers(0, 1000, (P, Q, k)).astype(np.uint64))
+    lc = rng.integers(0, k + 1, (P, Q)).astype(np.uint32)
+    oi, od, oc = bsr_mod.merge_top_k_lists(li, ld, lc, k)
+    for q in (0, 1, 1499, 2998, 2999):
+        ri, rd, rc = bsr_mod.merge_top_k_lists(li[:, q:q + 1], ld[:, q:q + 1], lc[:, q:q + 1], k)
+        assert oc[q] == rc[0] and np.array_equal(oi[q], ri[0]) and np.array_equal(od[q].view(np.uint32),
+                                                                                 rd[0].view(np.uint32))
