@@ -1,19 +1,27 @@
 """Benchmark: batched exact cosine top-k search (better-search-rag-rust's search hot path).
 
-Workload (BASELINE.json configs[1] per GPU): every rank holds a 1M-row shard of a synthetic
-768-d U(-1,1) f32 corpus (the shard is interval_by_rank(rank, N, N*1M) of one global corpus
-generated on the device), 1000 queries (query 0 = corpus row 0, the reference's self-query),
-top-10.  One step = parallel_top_k_similarity_search for the whole query batch: local search
-on every GPU (int8 MFMA candidate filter + exact f32 rescore), RCCL all-gather of the partial lists,
-host merge on rank 0.  Weak scaling: the corpus grows with N (1M rows per GPU); `value`
-counts each query once per 1M-row shard, so at N=1 it is plain queries/s over 1M vectors.
+Default workload (BASELINE.json configs[2], strong scaling): one synthetic corpus of 10M
+768-d U(-1,1) f32 rows (seed 42, generated on the devices), sharded over the N GPUs with the
+reference's interval_by_rank; 1000 queries (query 0 = corpus row 0, the reference's
+self-query), top-10.  One step = parallel_top_k_similarity_search for the whole batch:
+the local search on every GPU (int8 MFMA candidate filter + exact f32 rescore of the
+candidates, certified), the RCCL all-gather of the partial lists and the root's merge.
+`value` = queries/s over the whole 10M corpus (the same total work at every N).  At N = 1
+this is the north-star shape (batched 10M); the same run also reports configs[1] (the first
+1M rows, 1000 queries) and the single-query p50 over the full corpus (configs[3]).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  N > 1: launched by torch.distributed.run (one rank per GPU), or, without WORLD_SIZE in
+  the environment, bench.py starts the N rank processes itself (before any GPU call).
+  --comm host: the exchange over gloo instead of RCCL (ranks may then share a GPU: a
+  multi-rank rehearsal on a one-GPU box).
 """
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -26,6 +34,19 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 PEAK_BF16_DENSE = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
 PEAK_I8_DENSE = 5.0e15     # MI355X dense int8 MFMA: 2x the bf16 rate per clock (same guide)
 PEAK_HBM = 8.0e12          # MI355X HBM3E (spec)
+CPU_SHARE = 16             # host cores of one GPU's share on the box (nproc shows the machine)
+
+CONFIGS = {
+    # name: (rows in the corpus, queries, top-k, corpus dtype, sharding, label)
+    "c3": (10_000_000, 1000, 10, "f32", "strong",
+           "configs[2]: 10M x 768 f32 corpus sharded over the N GPUs, 1000 batched queries, top-10"),
+    "c2": (1_000_000, 1000, 10, "f32", "strong",
+           "configs[1]: 1M x 768 f32 corpus (sharded over the N GPUs), 1000 batched queries, top-10"),
+    "c4": (10_000_000, 1, 10, "f32", "strong",
+           "configs[3]: 10M x 768 f32 corpus, single queries (p50 path), top-10"),
+    "c5": (6_250_000, 4096, 100, "bf16", "weak",
+           "configs[4] per-GPU shard: 6.25M x 768 bf16 rows per GPU (50M over 8), 4096 queries, top-100"),
+}
 
 
 def parse():
@@ -33,49 +54,83 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000)
-    ap.add_argument("--queries", type=int, default=1000)
-    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
+    ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (tests)")
+    ap.add_argument("--queries", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl")
     ap.add_argument("--p50-iters", type=int, default=20)
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed searches before the warmup steps (setup): the GPU leaves its idle "
                          "clocks only after some ms of load, longer than a few warmup steps take")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per point of the CPU-baseline sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle (rank 0, N=1)")
+    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] side measurement (N=1)")
+    ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle on rank 0")
     ap.add_argument("--filter", choices=["i8", "bf16"], default="i8",
                     help="MFMA candidate-filter operand type (results are exact either way)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
-                    help="BASELINE.json configs: c2 = 1M f32 rows/GPU, 1000 queries, top-10 (the "
-                         "headline line); c4 = 10M rows, single queries, top-10 (p50 path); c5 = the "
-                         "per-GPU shard of 50M bf16 rows over 8 GPUs (6.25M), 4096 queries, top-100")
     a = ap.parse_args()
+    rows, q, k, dt, sc, label = CONFIGS[a.config]
+    a.rows_total = a.rows if a.rows is not None else rows
+    a.queries = a.queries if a.queries is not None else q
+    a.k = a.k if a.k is not None else k
+    a.corpus_dtype, a.scaling, a.label = dt, sc, label
     if a.config == "c4":
-        a.rows_per_gpu, a.queries, a.k = 10_000_000, 1, 10
         a.p50_iters = max(a.p50_iters, 100)
-    elif a.config == "c5":
-        a.rows_per_gpu, a.queries, a.k = 6_250_000, 4096, 100
     return a
+
+
+def spawn_ranks(n):
+    """Start the N rank processes (one per GPU) and wait; nothing here touches the GPU."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def main():
     args = parse()
-    import torch
-    import bsr
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+
+    import torch
+    import bsr
+
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap + timing only
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap, timing, host transport
+    ndev = torch.cuda.device_count()
+    device = local_rank % max(ndev, 1)
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
 
     def barrier():
         torch.cuda.synchronize()
@@ -83,15 +138,15 @@ def main():
             dist.barrier()
 
     D, Q, K = args.dim, args.queries, args.k
-    n_total = args.rows_per_gpu * world
+    n_total = args.rows_total * (world if args.scaling == "weak" else 1)
     iv = bsr.interval_by_rank(rank, world, n_total)
     start, n_local = iv.start_index, iv.get_count()
 
     # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index
     # (config 5: rounded to a bf16 corpus first; parity is on the widened bf16 values).
     fflag = bsr.BSR_FLAG_FILTER_BF16 if args.filter == "bf16" else 0
-    corpus_bf16 = args.config == "c5"
-    index = bsr.Index(D, max_k=max(K, 64), device=local_rank, flags=bsr.BSR_FLAG_PROFILE | fflag,
+    corpus_bf16 = args.corpus_dtype == "bf16"
+    index = bsr.Index(D, max_k=max(K, 64), device=device, flags=bsr.BSR_FLAG_PROFILE | fflag,
                       dtype=bsr.BSR_BF16 if corpus_bf16 else bsr.BSR_F32)
     shard = torch.empty((max(n_local, 1), D), dtype=torch.float32, device=dev)
     if n_local:
@@ -100,6 +155,11 @@ def main():
         shard = shard.to(torch.bfloat16)
     torch.cuda.synchronize()
     index.load(shard[:n_local] if n_local else np.zeros((0, D), np.float32), start)
+    # configs[1] side measurement (N = 1, default config): the first 1M rows of the corpus
+    ix1 = None
+    if world == 1 and args.config == "c3" and not args.no_configs1 and n_local >= 1_000_000:
+        ix1 = bsr.Index(D, max_k=64, device=device, flags=bsr.BSR_FLAG_PROFILE | fflag)
+        ix1.load(shard[:1_000_000], 0)
     del shard
     torch.cuda.empty_cache()
 
@@ -111,9 +171,12 @@ def main():
 
     comm = None
     if world > 1:
-        uid = [bsr.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = bsr.Comm(uid[0], rank, world, local_rank)
+        if args.comm == "host":
+            comm = bsr.Comm.host(dist.group.WORLD)
+        else:
+            uid = [bsr.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = bsr.Comm(uid[0], rank, world, device)
 
     lib = bsr.lib()
     oi = np.empty((Q, K), np.uint64)
@@ -121,32 +184,36 @@ def main():
     oc = np.empty(Q, np.uint32)
     comm_h = comm._h if comm else None
 
-    def step(nq=Q, qptr=None):
-        st = lib.bsr_parallel_top_k_similarity_search(comm_h, index._h, qptr or qdev.data_ptr(), nq, K,
-                                                       oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+    def step(nq=Q, qptr=None, ix=index):
+        st = lib.bsr_parallel_top_k_similarity_search(comm_h if ix is index else None, ix._h, qptr or qdev.data_ptr(),
+                                                       nq, K, oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
         if st != 0:
             raise bsr.BsrError(st, lib.bsr_last_error().decode())
+
+    def bcast_int(v):
+        if dist:
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.broadcast(t, src=0)
+            v = int(t.item())
+        return v
 
     # Clock settle: the same number of untimed searches on every rank (each search is a
     # collective for N > 1), sized on rank 0 from one search's time.
     step()
     t1 = time.perf_counter()
     step()
-    n_settle = int(args.settle_ms * 1e-3 / max(time.perf_counter() - t1, 1e-5)) if args.settle_ms > 0 else 0
-    if dist:
-        nt = torch.tensor([n_settle], dtype=torch.int64)
-        dist.broadcast(nt, src=0)
-        n_settle = int(nt.item())
+    n_settle = bcast_int(int(args.settle_ms * 1e-3 / max(time.perf_counter() - t1, 1e-5)) if args.settle_ms > 0 else 0)
     for _ in range(n_settle):
         step()
     for _ in range(args.warmup):
         step()
     barrier()
-    # Timed region: HIP events on the filter kernels only (the roofline's launch durations);
-    # the per-stage breakdown comes from a separate profiled pass below.
+    # Timed region: exactly K searches between barriers; HIP events on the filter kernels
+    # only (bound to their dispatch: the roofline's launch durations).
     index.set_profile(1)
     index.profile(reset=True)
     stats_fb = 0
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -154,25 +221,21 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     prof = index.profile(reset=True)
-    index.set_profile(2)
-    n_stage = max(3, min(args.steps, 10))
-    for _ in range(n_stage):
-        step()
-    prof_st = index.profile(reset=True)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
     st = index.last_stats()
+    res_i, res_d, res_c = oi.copy(), od.copy(), oc.copy()  # the last timed step's result (root)
+    # per-stage breakdown from a separate profiled pass (every stage evented)
+    index.set_profile(2)
+    n_stage = max(3, min(args.steps, 10))
+    for _ in range(n_stage):
+        step()
+    prof_st = index.profile(reset=True)
 
-    # Self-query check of the reference's driver (src/main.rs:141-154): row 0 ranks first.
-    self_ok = None
-    if rank == 0:
-        self_ok = bool(oi[0, 0] == 0 and od[0, 0] == 0.0)
-
-    # p50 single-query latency (config 4 style path: exact HBM-bound scan), all ranks.
-    # Latency without event recording; the kernel breakdown from a separate profiled pass.
+    # p50 single-query latency over the whole corpus (configs[3] path), all ranks.
     lat = []
     index.set_profile(0)
     for _ in range(args.p50_iters):
@@ -187,52 +250,68 @@ def main():
         step(1, qdev[1:2].data_ptr())
     prof_scan = index.profile(reset=True)
 
+    # configs[1] side measurement (N = 1): 1M rows, the same 1000 queries
+    c1 = None
+    if ix1 is not None:
+        for _ in range(max(args.warmup, 3) + 20):
+            step(ix=ix1)
+        ix1.set_profile(1)
+        ix1.profile(reset=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(ix=ix1)
+        torch.cuda.synchronize()
+        c1_ms = (time.perf_counter() - t1) / args.steps * 1e3
+        p1 = ix1.profile(reset=True)
+        e1 = p1.gemm_emit_ms / max(p1.gemm_emit_launches, 1)
+        a1 = 2.0 * Q * 1_000_000 * D / (e1 * 1e-3) if e1 > 0 else None
+        c1 = {"workload": "configs[1]: first 1M rows of the corpus, the same 1000 queries, top-10, 1 GPU",
+              "value": round(Q / (c1_ms * 1e-3), 2), "unit": "queries/s", "ms_per_step": round(c1_ms, 4),
+              "filter_avg_launch_ms": round(e1, 5),
+              "filter_frac_of_i8_peak": round(a1 / PEAK_I8_DENSE, 4) if a1 and args.filter == "i8" else None}
+        step()  # leave oi/od as the main index's
+        ix1.close()
+        ix1 = None
+
     out = None
+    nk = (D + 63) // 64
     if rank == 0:
         launches = max(prof.gemm_emit_launches, 1)
         emit_ms = prof.gemm_emit_ms / launches
-        flops = 2.0 * Q * n_local * D
-        achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
         traffic = None
-        peak = PEAK_I8_DENSE if args.filter == "i8" else PEAK_BF16_DENSE
-        nk = (D + 63) // 64
-        if args.filter == "i8":
-            kname = f"k_filter_qs8<true, {nk}>" if nk % 2 == 0 and nk <= 12 else "k_filter<OpI8, true>"
-        else:
-            kname = "k_filter<OpBF16, true>"
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
                 if pm.get("rows") == n_local and pm.get("queries") == Q and pm.get("filter") == args.filter:
                     traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
+            except (OSError, ValueError):
                 traffic = None
-        value = (Q * world if args.config == "c2" else Q) / (ms_per_step * 1e-3)
-        # Batches of <= 16 queries on an int8 index run the skinny filter (csrc/index.cpp,
-        # kSkinnyMaxQ): HBM-bound, its roofline is the int8 rows streamed once per launch.
-        skinny = args.filter == "i8" and Q <= 16
-        if skinny:
+        if args.filter == "i8" and Q <= 16:
+            # <= 16 queries on an int8 index: the skinny filter (HBM-bound)
             kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
             kname = f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>"
             sbytes = n_local * nk * 64
-            sgbs = sbytes / (emit_ms * 1e-3) / 1e9 if emit_ms > 0 else None
-            roof = {"bound": "hbm", "kernel": kname, "achieved": round(sgbs, 1) if sgbs else None,
-                    "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(sgbs * 1e9 / PEAK_HBM, 4) if sgbs else None,
+            gbs = sbytes / (emit_ms * 1e-3) / 1e9 if emit_ms > 0 else None
+            roof = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1) if gbs else None,
+                    "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4) if gbs else None,
                     "traffic": traffic, "algorithmic_bytes_per_launch": sbytes, "avg_launch_ms": round(emit_ms, 5)}
         else:
-            roof = {
-                "bound": "mfma", "kernel": kname,
-                "achieved": round(achieved, 2) if achieved else None,
-                "peak": peak / 1e12, "unit": "TOP/s" if args.filter == "i8" else "TFLOP/s",
-                "frac": round(achieved * 1e12 / peak, 4) if achieved else None,
-                "frac_of_bf16_peak": round(achieved * 1e12 / PEAK_BF16_DENSE, 4) if achieved else None,
-                "traffic": traffic,
-                "algorithmic_flops_per_launch": flops,
-                "avg_launch_ms": round(emit_ms, 5),
-            }
+            flops = 2.0 * Q * n_local * D
+            achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
+            peak = PEAK_I8_DENSE if args.filter == "i8" else PEAK_BF16_DENSE
+            if args.filter == "i8":
+                kname = f"k_filter_qs8<true, {nk}>" if nk % 2 == 0 and nk <= 12 else "k_filter<OpI8, true>"
+            else:
+                kname = "k_filter<OpBF16, true>"
+            roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2) if achieved else None,
+                    "peak": peak / 1e12, "unit": "TOP/s" if args.filter == "i8" else "TFLOP/s",
+                    "frac": round(achieved * 1e12 / peak, 4) if achieved else None, "traffic": traffic,
+                    "algorithmic_ops_per_launch": flops, "avg_launch_ms": round(emit_ms, 5),
+                    "note": "rank 0's shard; ops = 2 * queries * shard rows * dim (int8 multiply-adds)"}
         out = {
             "metric": "queries/sec + p50 latency, 768-d top-10 over N vectors @1/2/4/8 GPU",
-            "value": round(value, 2),
+            "value": round(Q / (ms_per_step * 1e-3), 2),
             "unit": "queries/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -240,96 +319,132 @@ def main():
             "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": args.filter,
+            "dtype": "f32",
+            "filter_dtype": args.filter,
             "data": f"synthetic U(-1,1) {'bf16' if corpus_bf16 else 'f32'} corpus generated on device (seed 42), "
-                    f"{Q} queries (seed 43, query 0 = row 0)",
+                    f"{Q} queries (seed 43, query 0 = row 0), HBM-resident",
             "config": {
-                "workload": {"c2": "configs[1] per GPU", "c4": "configs[3] (single-query path)",
-                             "c5": "configs[4] per-GPU shard"}[args.config] +
-                            f": {n_local} x {D} {'bf16' if corpus_bf16 else 'f32'} rows per GPU ({n_total} total), "
-                            f"{Q} batched queries, top-{K}" +
-                            ("; value = queries x 1M-row shards / s" if args.config == "c2" else "; value = queries / s"),
-                "rows_total": n_total, "rows_per_gpu": n_local, "queries": Q, "top_k": K, "dim": D,
-                "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank) + RCCL all-gather",
+                "workload": args.label + ("" if args.rows is None else f" (rows overridden: {n_total})"),
+                "rows_total": n_total, "rows_per_gpu_rank0": n_local, "queries": Q, "top_k": K, "dim": D,
+                "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank)" +
+                               ("" if world == 1 else f" + {args.comm.upper()} all-gather of the partial lists"
+                                                      " + root merge"),
                 "filter": ("int8 MFMA (v_mfma_i32_32x32x32_i8) candidates" if args.filter == "i8" else
                            "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates") +
                           f", exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)",
-                "qps_over_full_corpus": round(Q / (ms_per_step * 1e-3), 2),
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
-            "p50_config": f"1 query over {n_total} rows" + (
-                " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else " (exact f32 scan, HBM-bound)"),
+            "p50_config": f"1 query over {n_total} rows on {world} GPU(s)" + (
+                " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else
+                " (exact f32 scan, HBM-bound)"),
             "roofline": roof,
-            "kernels_ms_per_step": {  # separate profiled pass of n_stage steps (every stage evented)
-                "gemm_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
-                "gemm_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
+            "kernels_ms_per_step_rank0": {  # separate profiled pass of n_stage steps (every stage evented)
+                "filter_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
+                "filter_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
                 "select": round(prof_st.select_ms / n_stage, 4),
                 "rescore": round(prof_st.rescore_ms / n_stage, 4),
                 "scan_fallback": round(prof_st.scan_ms / n_stage, 4),
-                "local_search_total": round(prof_st.search_ms / n_stage, 4),
-            },
-            "p50_kernels_ms": {
+                "local_search_total": round(prof_st.search_ms / n_stage, 4)},
+            "p50_kernels_ms_rank0": {
                 "filter_emit": round(prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1), 4),
                 "filter_sample": round(prof_scan.gemm_sample_ms / max(prof_scan.gemm_sample_launches, 1), 4),
                 "exact_scan": round(prof_scan.scan_ms / max(prof_scan.scan_launches, 1), 4),
                 "local_search_total": round(prof_scan.search_ms / max(prof_scan.searches, 1), 4)},
-            "fallback_queries_per_step": stats_fb / args.steps,
+            "fallback_queries_per_step_rank0": stats_fb / args.steps,
             "candidates_per_query": st.n_candidates,
-            "self_query_rank1": self_ok,
-            "emitted_per_query": round(st.n_emitted / max(Q, 1), 1),
+            "self_query_rank1": bool(res_i[0, 0] == 0 and res_d[0, 0] == 0.0),
+            "emitted_per_query_rank0": round(st.n_emitted / max(Q, 1), 1),
             "row_ebound": round(float(st.row_ebound), 6),
         }
-        # HBM roofline of the single-query (p50) kernel: the int8 skinny filter reads the
-        # int8 rows (N*ld bytes per query batch); the bf16 index uses the exact f32 scan
-        # (N*ld*4 bytes).
-        if args.filter == "i8":
-            kms = prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1)
-            nk = (D + 63) // 64
-            kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
-            kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>")
-        else:
-            kms = prof_scan.scan_ms / max(prof_scan.scan_launches, 1)
-            kbytes, kn = n_local * ((D + 63) // 64 * 64) * 4, "k_scan_exact<1,1>"
+        if c1:
+            out["configs1"] = c1
+        kms = (prof_scan.gemm_emit_ms / max(prof_scan.gemm_emit_launches, 1) if args.filter == "i8" else
+               prof_scan.scan_ms / max(prof_scan.scan_launches, 1))
         if kms > 0:
+            if args.filter == "i8":
+                kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
+                kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>")
+            else:
+                kbytes, kn = n_local * nk * 64 * 4, "k_scan_exact<1,1>"
             gbs = kbytes / (kms * 1e-3) / 1e9
-            out["roofline_p50"] = {"bound": "hbm", "kernel": kn, "achieved": round(gbs, 1),
-                                   "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4),
-                                   "bytes_per_launch": kbytes, "avg_launch_ms": round(kms, 4)}
+            out["roofline_p50"] = {"bound": "hbm", "kernel": kn, "achieved": round(gbs, 1), "peak": PEAK_HBM / 1e9,
+                                   "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4), "bytes_per_launch": kbytes,
+                                   "avg_launch_ms": round(kms, 4)}
 
-    # Parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on the same corpus.
-    if rank == 0 and world == 1 and (args.verify or not args.no_cpu_baseline):
+    # Parity spot-check on rank 0 at every N, against the oracle over the WHOLE corpus:
+    # the corpus is regenerated 1M rows at a time on rank 0's GPU (the same counter-based
+    # generator), each block's oracle lists merged as the reference merges rank blocks.
+    # Then the CPU baseline (rank 0, N = 1).  Other ranks wait at the final barrier.
+    if rank == 0 and (args.verify or (world == 1 and not args.no_cpu_baseline)):
         import oracle
-        rows_h = index.get_many()
         q_h = qdev.cpu().numpy()
+        chunk = 1_000_000
+        buf = torch.empty((min(chunk, n_total), D), dtype=torch.float32, device=dev)
+
+        def corpus_block(r0, n):
+            bsr.synth_uniform(buf.data_ptr(), r0, n, D, 42)
+            torch.cuda.synchronize()
+            blk = buf[:n]
+            if corpus_bf16:
+                blk = blk.to(torch.bfloat16).to(torch.float32)
+            return blk.cpu().numpy()
+
+        threads = max(1, min(CPU_SHARE, os.cpu_count() or 1))
+        first_block = None
         if args.verify:
             nv = min(args.verify, Q)
-            step()  # refresh oi/od for the full batch
-            wi, wd, wc = oracle.parallel_top_k(rows_h, q_h[:nv], K, size=min(16, os.cpu_count() or 1),
-                                               threads=min(16, os.cpu_count() or 1))
+            t_v = time.perf_counter()
+            parts_i, parts_d = [[] for _ in range(nv)], [[] for _ in range(nv)]
+            for r0 in range(0, n_total, chunk):
+                n = min(chunk, n_total - r0)
+                rows_h = corpus_block(r0, n)
+                if r0 == 0:
+                    first_block = rows_h
+                wi, wd, wc = oracle.parallel_top_k(rows_h, q_h[:nv], K, size=threads, threads=threads)
+                for q in range(nv):
+                    parts_i[q].append(wi[q, :wc[q]] + np.uint64(r0))
+                    parts_d[q].append(wd[q, :wc[q]])
+            ok_i = ok_d = True
+            for q in range(nv):
+                gi, gd = oracle.global_top_k(np.concatenate(parts_i[q]), np.concatenate(parts_d[q]), K)
+                c = int(res_c[q])
+                ok_i &= c == len(gi) and np.array_equal(res_i[q, :c], gi)
+                ok_d &= c == len(gd) and np.array_equal(res_d[q, :c].view(np.uint32), gd.view(np.uint32))
             out["parity_spot_check"] = {
-                "queries": nv,
-                "indices_equal": bool(np.array_equal(oi[:nv], wi)),
-                "distance_bits_equal": bool(np.array_equal(od[:nv].view(np.uint32), wd.view(np.uint32))),
-            }
-        if not args.no_cpu_baseline:
-            threads = max(1, min(16, os.cpu_count() or 1))
-            t1 = time.perf_counter()
-            oracle.parallel_top_k(rows_h, q_h[1:2], K, size=threads, threads=threads)
-            one = time.perf_counter() - t1
-            nq_cpu = max(1, min(Q, int(args.cpu_seconds / max(one, 1e-3))))
-            t1 = time.perf_counter()
-            oracle.parallel_top_k(rows_h, q_h[:nq_cpu], K, size=threads, threads=threads)
-            cpu_t = time.perf_counter() - t1
+                "queries": nv, "rows": n_total, "indices_equal": bool(ok_i), "distance_bits_equal": bool(ok_d),
+                "method": f"oracle (oracle/bsr_oracle.c) over the regenerated corpus in {chunk}-row blocks, "
+                          f"merged with compute_global_top_k; {time.perf_counter() - t_v:.1f} s"}
+        if world == 1 and not args.no_cpu_baseline:
+            # P = 1, 2, 4, 8, 16 rank threads (the mpiexec analogue), each on a bounded sample:
+            # the first 1M rows (the reference's per-row cost is linear in rows), queries
+            # scaled per P to ~cpu_seconds; reported as queries/s over the full corpus.
+            rows_s = first_block if first_block is not None else corpus_block(0, min(chunk, n_total))
+            n_s = rows_s.shape[0]
+            sweep = []
+            for P in [p for p in (1, 2, 4, 8, 16) if p <= threads]:
+                t1 = time.perf_counter()
+                oracle.parallel_top_k(rows_s, q_h[1:2], K, size=P, threads=P)
+                one = time.perf_counter() - t1
+                nq_cpu = max(1, min(Q, int(args.cpu_seconds / max(one, 1e-3))))
+                t1 = time.perf_counter()
+                oracle.parallel_top_k(rows_s, q_h[:nq_cpu], K, size=P, threads=P)
+                dt = time.perf_counter() - t1
+                sweep.append({"P": P, "queries": nq_cpu, "seconds": round(dt, 3),
+                              "qps_full_corpus": round(nq_cpu / dt * n_s / n_total, 4)})
+            best = max(sweep, key=lambda s: s["qps_full_corpus"])
             out["cpu_baseline"] = {
-                "value": round(nq_cpu / cpu_t, 4), "unit": "queries/s", "cores": threads, "kind": "port",
-                "sample": f"{nq_cpu} of the {Q} queries over the same {n_local}-row corpus, "
-                          f"{threads} rank threads (mpiexec analogue), oracle/bsr_oracle.c",
-            }
-        else:
+                "value": best["qps_full_corpus"], "unit": "queries/s", "cores": best["P"], "kind": "port",
+                "sample": f"oracle/bsr_oracle.c (the reference path restated: per-rank block scan + stable "
+                          f"sort, rank-order gather, stable sort + dedupe) with P rank threads over the first "
+                          f"{n_s} rows of the corpus, {best['queries']} queries at the best P; queries/s over "
+                          f"{n_total} rows = measured x {n_s}/{n_total}",
+                "sweep": sweep, "nproc": os.cpu_count(), "cpu_share": CPU_SHARE, "cpu_model": cpu_model()}
+        elif world == 1:
             out["cpu_baseline"] = None
     if rank == 0:
+        out.setdefault("cpu_baseline", None)  # N > 1: the baseline is measured at N = 1 only
         print(json.dumps(out), flush=True)
     barrier()
     if comm:

@@ -1,0 +1,218 @@
+"""GPU parity at BASELINE.json's full sizes (configs[1]-[4]), through the C ABI.
+
+Every query of a batch is checked by size-independent properties (counts, (distance, index)
+order, no fallback, self-query first, idempotence, shard-count independence); a subset of
+queries is checked bit for bit against the oracle over the WHOLE corpus, computed block by
+block (<= 1M rows at a time, the corpus regenerated on the GPU by the same counter-based
+generator the index was loaded from) and merged as the reference merges rank blocks
+(oracle.global_top_k of the rank-order concatenation).  Oracle time stays at seconds.
+
+Sizes: configs[1] 1M x 1000 (top-10); configs[2] 10M as the 8 interval_by_rank shards of
+8 GPUs, loaded one at a time with their global offsets, and as one 10M shard; configs[3]
+10M x single queries (the skinny path, graph replay); configs[4] the 6.25M-row bf16 shard
+of 50M over 8 GPUs x 4096 queries, top-100 (4.8 GB of int8 filter rows: row offsets past
+4 GiB)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+D = 768
+CHUNK = 1_000_000
+THREADS = max(1, min(16, os.cpu_count() or 1))
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _gen(bsr_mod, n, row0=0, seed=42, bf16=False):
+    """Rows [row0, row0+n) of the synthetic corpus on the GPU (f32, or bf16-rounded)."""
+    torch = _torch()
+    t = torch.empty((n, D), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(t.data_ptr(), row0, n, D, seed)
+    torch.cuda.synchronize()
+    return t.to(torch.bfloat16) if bf16 else t
+
+
+def _queries(bsr_mod, nq, plant=()):
+    """nq seed-43 queries; query i of `plant` (position, corpus row) is that corpus row."""
+    torch = _torch()
+    q = torch.empty((nq, D), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(q.data_ptr(), 0, nq, D, 43)
+    for pos, row in plant:
+        bsr_mod.synth_uniform(q[pos:pos + 1].data_ptr(), row, 1, D, 42)
+    torch.cuda.synchronize()
+    return q
+
+
+def _chunked_oracle(bsr_mod, oracle_mod, n_total, qs_h, k, bf16=False):
+    """The reference's answer over n_total corpus rows for queries qs_h, 1M rows at a time."""
+    torch = _torch()
+    nv = qs_h.shape[0]
+    parts_i, parts_d = [[] for _ in range(nv)], [[] for _ in range(nv)]
+    for r0 in range(0, n_total, CHUNK):
+        n = min(CHUNK, n_total - r0)
+        blk = _gen(bsr_mod, n, r0, bf16=bf16)
+        rows = (blk.to(torch.float32) if bf16 else blk).cpu().numpy()
+        del blk
+        wi, wd, wc = oracle_mod.parallel_top_k(rows, qs_h, k, size=THREADS, threads=THREADS)
+        for q in range(nv):
+            parts_i[q].append(wi[q, :wc[q]] + np.uint64(r0))
+            parts_d[q].append(wd[q, :wc[q]])
+    out_i = np.zeros((nv, k), np.uint64)
+    out_d = np.zeros((nv, k), np.float32)
+    out_c = np.zeros(nv, np.uint32)
+    for q in range(nv):
+        gi, gd = oracle_mod.global_top_k(np.concatenate(parts_i[q]), np.concatenate(parts_d[q]), k)
+        out_i[q, :len(gi)], out_d[q, :len(gd)], out_c[q] = gi, gd, len(gi)
+    return out_i, out_d, out_c
+
+
+def _search_device(ix, q, k):
+    torch = _torch()
+    nq = q.shape[0]
+    oi = torch.empty((nq, k), dtype=torch.int64, device="cuda:0")
+    od = torch.empty((nq, k), dtype=torch.float32, device="cuda:0")
+    oc = torch.empty(nq, dtype=torch.int32, device="cuda:0")
+    ix.local_top_k_device(q, nq, k, oi, od, oc)
+    return oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32)
+
+
+def _check_properties(got, n, k, ctx):
+    gi, gd, gc = got
+    assert (gc == min(k, n)).all(), (ctx, np.unique(gc))
+    c = int(min(k, n))
+    assert (gi[:, :c] < n).all(), ctx
+    assert ((gd[:, :c] >= 0) & (gd[:, :c] <= 2)).all(), ctx
+    # (distance asc, index asc) order on every query
+    d, i = gd[:, :c], gi[:, :c].astype(np.int64)
+    ok = (d[:, 1:] > d[:, :-1]) | ((d[:, 1:] == d[:, :-1]) & (i[:, 1:] > i[:, :-1]))
+    assert ok.all(), (ctx, np.argwhere(~ok)[:4])
+
+
+def _assert_same(got, want, rows, ctx):
+    gi, gd, gc = got
+    wi, wd, wc = want
+    for j, q in enumerate(rows):
+        c = int(wc[j])
+        assert gc[q] == c, (ctx, q)
+        assert np.array_equal(gi[q, :c], wi[j, :c]), (ctx, q, gi[q, :c], wi[j, :c])
+        assert np.array_equal(gd[q, :c].view(np.uint32), wd[j, :c].view(np.uint32)), (ctx, q)
+
+
+# ---- configs[1]: 1M x 1000, top-10 ----------------------------------------------------------
+def test_configs1_1m_x_1000(bsr_mod, oracle_mod, gpu):
+    n, nq, k = 1_000_000, 1000, 10
+    rows = _gen(bsr_mod, n)
+    ix = bsr_mod.Index(D, max_k=k, device=0)
+    ix.load(rows, 0)
+    del rows
+    q = _queries(bsr_mod, nq, plant=[(0, 0), (500, 999_999), (999, 654_321)])
+    got = _search_device(ix, q, k)
+    st = ix.last_stats()
+    assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
+    _check_properties(got, n, k, "configs[1]")
+    for pos, row in ((0, 0), (500, 999_999), (999, 654_321)):
+        assert got[0][pos, 0] == row and got[1][pos, 0] == 0.0
+    again = _search_device(ix, q, k)  # idempotent
+    assert all(np.array_equal(a, b) for a, b in zip(got, again))
+    sub = [0, 1, 2, 500, 733, 998, 999]
+    want = _chunked_oracle(bsr_mod, oracle_mod, n, q[sub].cpu().numpy(), k)
+    _assert_same(got, want, sub, "configs[1] vs oracle")
+    ix.close()
+
+
+# ---- configs[2] and configs[3]: 10M ---------------------------------------------------------
+@pytest.fixture(scope="module")
+def index_10m(bsr_mod, gpu):
+    n = 10_000_000
+    rows = _gen(bsr_mod, n)
+    ix = bsr_mod.Index(D, max_k=16, device=0)
+    ix.load(rows, 0)
+    del rows
+    _torch().cuda.empty_cache()
+    yield ix, n
+    ix.close()
+
+
+def test_configs2_10m_x_1000_shards_and_whole(bsr_mod, oracle_mod, index_10m):
+    """configs[2]: the 8 shards of 10M (interval_by_rank(r, 8, 10M), 1.25M rows each, global
+    offsets) searched one at a time and merged by the library's root merge == one 10M shard,
+    on all 1000 queries; 6 queries bit for bit vs the oracle over all 10M rows."""
+    ix10, n = index_10m
+    nq, k, P = 1000, 10, 8
+    q = _queries(bsr_mod, nq, plant=[(0, 0), (1, n - 1), (2, 5_600_000), (3, 1_250_000)])
+    whole = _search_device(ix10, q, k)
+    assert ix10.last_stats().n_fallback == 0
+    _check_properties(whole, n, k, "10M whole")
+    li = np.zeros((P, nq, k), np.uint64)
+    ld = np.zeros((P, nq, k), np.float32)
+    lc = np.zeros((P, nq), np.uint32)
+    for r in range(P):
+        iv = bsr_mod.interval_by_rank(r, P, n)
+        s, cnt = iv.start_index, iv.get_count()
+        rows = _gen(bsr_mod, cnt, s)
+        ix = bsr_mod.Index(D, max_k=k, device=0)
+        ix.load(rows, s)
+        del rows
+        li[r], ld[r], lc[r] = _search_device(ix, q, k)
+        assert ix.last_stats().n_fallback == 0
+        assert ((li[r] >= s) & (li[r] < s + cnt)).all()
+        ix.close()
+        _torch().cuda.empty_cache()
+    merged = bsr_mod.merge_top_k_lists(li, ld, lc, k)
+    assert all(np.array_equal(a, b) for a, b in zip(merged, whole)), "8 shards != 1 shard"
+    for pos, row in ((0, 0), (1, n - 1), (2, 5_600_000), (3, 1_250_000)):
+        assert whole[0][pos, 0] == row and whole[1][pos, 0] == 0.0
+    sub = [0, 1, 2, 3, 4, 999]
+    want = _chunked_oracle(bsr_mod, oracle_mod, n, q[sub].cpu().numpy(), k)
+    _assert_same(whole, want, sub, "configs[2] vs oracle")
+
+
+def test_configs3_10m_single_queries(bsr_mod, oracle_mod, index_10m):
+    """configs[3]: single queries over 10M rows (the skinny HBM-bound filter, then captured
+    graph replays), each bit for bit vs the oracle over all 10M rows."""
+    ix10, n = index_10m
+    k = 10
+    q = _queries(bsr_mod, 4, plant=[(0, 0), (3, n - 2)])
+    qs_h = q.cpu().numpy()
+    want = _chunked_oracle(bsr_mod, oracle_mod, n, qs_h, k)
+    replays = 0
+    for rep in range(3):
+        for j in range(4):
+            got = ix10.local_top_k(qs_h[j:j + 1], k)
+            st = ix10.last_stats()
+            assert st.n_fallback == 0
+            replays += st.graph_replay
+            _assert_same(got, tuple(w[j:j + 1] for w in want), [0], f"configs[3] q{j} rep{rep}")
+    assert replays > 0
+    assert want[0][0, 0] == 0 and want[0][3, 0] == n - 2
+
+
+# ---- configs[4]: 6.25M bf16 rows (one of 8 shards of 50M) x 4096, top-100 --------------------
+def test_configs4_bf16_shard_x_4096_top100(bsr_mod, oracle_mod, gpu):
+    n, nq, k = 6_250_000, 4096, 100
+    rows = _gen(bsr_mod, n, bf16=True)
+    ix = bsr_mod.Index(D, max_k=k, device=0, dtype=bsr_mod.BSR_BF16)
+    ix.load(rows, 0)
+    del rows
+    _torch().cuda.empty_cache()
+    torch = _torch()
+    q = _gen(bsr_mod, nq, 0, seed=43)
+    for pos, row in ((0, 0), (1, n - 1), (2, 6_000_000)):   # rows past 4 GiB of int8 operand
+        q[pos] = _gen(bsr_mod, 1, row, bf16=True).to(torch.float32)[0]
+    torch.cuda.synchronize()
+    got = _search_device(ix, q, k)
+    st = ix.last_stats()
+    assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
+    _check_properties(got, n, k, "configs[4]")
+    for pos, row in ((0, 0), (1, n - 1), (2, 6_000_000)):
+        assert got[0][pos, 0] == row and got[1][pos, 0] == 0.0
+    sub = [0, 1, 2, 3, 2048, 4095]
+    want = _chunked_oracle(bsr_mod, oracle_mod, n, q[sub].cpu().numpy(), k, bf16=True)
+    _assert_same(got, want, sub, "configs[4] vs oracle")
+    ix.close()

@@ -2,7 +2,7 @@
 // ablations on a synthetic shard.  Includes the product kernel source directly.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../../include -I../../better-search-rag-rust_amd/csrc gemm_ablate.hip -o gemm_ablate
 // Run: ./gemm_ablate [rows] [queries] [rounds] [variant-substring]
-#include "k_filter.hip"
+#include "k_filter_lab.hip"
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
