@@ -301,7 +301,7 @@ def main():
             achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
             peak = PEAK_I8_DENSE if args.filter == "i8" else PEAK_BF16_DENSE
             if args.filter == "i8":
-                kname = f"k_filter_qs8<true, {nk}>" if nk % 2 == 0 and nk <= 12 else "k_filter<OpI8, true>"
+                kname = f"k_filter_qs16<true, {nk}>" if nk % 2 == 0 and nk <= 12 else "k_filter<OpI8, true>"
             else:
                 kname = "k_filter<OpBF16, true>"
             roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2) if achieved else None,

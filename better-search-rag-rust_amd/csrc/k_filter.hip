@@ -95,20 +95,10 @@ __device__ __forceinline__ void mid_barrier() {
 // The first MFMA group of every tile takes a zero C operand, so the accumulators are never
 // cleared by vector moves (all eight waves reach the epilogue together, so anything done
 // there is not hidden behind another wave's MFMAs).
-//
-// VAR (tooling, tools/microbench): 1 = no LDS-DMA in the loop (compute ceiling),
-// 3 = LDS-DMA, waits and barriers only (operand-feed ceiling), 4 = A always the same tile,
-// 5 = no epilogue (accumulators kept live), 6 = neither LDS-DMA nor epilogue.
-// STAMP (tooling): thread 0 of each workgroup writes its s_memtime / s_memrealtime deltas
-// to S (in-kernel clock, MI355X_MICROARCH.md 'DVFS give-back' item 6).
-// EPI (tooling): 0 = the previous epilogue (per-lane mask over all 16 registers of a block
-// whose maximum passes, explicit clears), 1 = that epilogue with zero-C first MFMAs.
+// (Ablation variants of this kernel live in tools/microbench/k_filter_lab.hip.)
 // ------------------------------------------------------------------------------------
-template <class Op, bool EMIT, int VAR = 0, bool STAG = false, bool PRIO = false, int EPI = 2, bool STAMP = false>
+template <class Op, bool EMIT>
 __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
-    constexpr bool kNoDMA = VAR == 1 || VAR == 6, kNoMath = VAR == 3 || VAR == 4, kNoEpi = VAR == 5 || VAR == 6;
-    uint64_t t0 = 0, r0 = 0;
-    if (STAMP) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
     using frag_t = typename Op::frag_t;
     using acc_t = typename Op::acc_t;
     constexpr int BM = kFilterTile, BN = kFilterTile;
@@ -159,7 +149,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
     uint32_t iss_ti = 0, iss_kt = 0;
     __amdgpu_buffer_rsrc_t rsrc_a = rsrc_b;
     auto set_issue_tile = [&]() {
-        const uint32_t rt = VAR == 4 ? g0 : g0 + iss_ti * RG;
+        const uint32_t rt = g0 + iss_ti * RG;
         rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
                                                    BM * (uint32_t)p.a_stride, 0x00020000);
         if (!EMIT) {  // sample pass: tail rows read the last valid row
@@ -219,16 +209,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 
     frag_t fa0[4], fb0[2], fa1[4], fb1[2];
     auto read_frags = [&](uint32_t jj, int kk, frag_t (&fa)[4], frag_t (&fb)[2]) {
-        if constexpr (kNoMath) return;
-        const uint8_t* base = lds + (kNoDMA ? 0 : jj % kSlots) * SLOT;
+        const uint8_t* base = lds + (jj % kSlots) * SLOT;
 #pragma unroll
         for (int m = 0; m < 4; ++m) fa[m] = *reinterpret_cast<const frag_t*>(base + aoff[m][kk]);
 #pragma unroll
         for (int n = 0; n < 2; ++n) fb[n] = *reinterpret_cast<const frag_t*>(base + boff[n][kk]);
     };
     auto mfma4 = [&](const frag_t (&fa)[4], const frag_t (&fb)[2], int half, bool first) {
-        if constexpr (kNoMath) return;
-        if (EPI >= 1 && first) {  // first K step of a tile: C = 0
+        if (first) {  // first K step of a tile: C = 0
             const acc_t z = {};
 #pragma unroll
             for (int m = half * 2; m < half * 2 + 2; ++m)
@@ -248,9 +236,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         else return v;
     };
 
-    // PRIO: static priority for the second-dispatched half (waves 4-7, the arbitration
-    // losers of every segment; MI355X_MICROARCH.md "Two waves per SIMD", item 4).
-    if (PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
     // Prologue: slices 0..min(J,3)-1 issued; wait for slice 0; F0 <- (0, kk=0).
     set_issue_tile();
     const uint32_t pre = J < 3 ? J : 3;
@@ -266,26 +251,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
 
     uint32_t ti = 0, kt = 0;
     for (uint32_t jj = 0; jj < J; ++jj) {
-        const bool iss = !kNoDMA && jj + 3 < J;
+        const bool iss = jj + 3 < J;
         // ---- first half: kk = 0 MFMAs, kk = 1 reads, A-half DMA of slice jj+3.  The
         // reads go after the first MFMA group: hipcc puts a conservative lgkmcnt(0) in
         // front of an MFMA whose operands came from ds_read (it cannot see the barrier's
         // inline wait), which must not cover reads issued just before it.
-        // STAG: the wr=1 waves (the SIMD partners of the wr=0 waves) issue each DMA before
-        // the MFMA group instead of after it, so one partner's DMA issue overlaps the other
-        // partner's MFMAs (the per-wave DMA count before each barrier is unchanged).
-        const bool stag = STAG && wr == 1;
-        if (stag && iss) dma_a(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa0, fb0, 0, kt == 0);
         __builtin_amdgcn_sched_barrier(0);
         read_frags(jj, 1, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) { if (stag) dma_a(jj + 3, 1); else dma_a(jj + 3, 0); }
+        if (iss) dma_a(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa0, fb0, 1, kt == 0);
         __builtin_amdgcn_sched_barrier(0);
-        if (!stag && iss) dma_a(jj + 3, 1);
+        if (iss) dma_a(jj + 3, 1);
         if constexpr (kScaleDMA) {
             // this wave's 4 block scales of the current tile (rows rt*256 + wr*128 + 32m);
             // younger than every slice DMA in flight, so covered two mid-barriers later
@@ -296,9 +276,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- mid-slice barrier: slice jj+1 has landed for every wave
-        if (kNoDMA) {
-            mid_barrier<8>();
-        } else if (jj + 3 < J) {
+        if (jj + 3 < J) {
             mid_barrier<6>();
         } else if (jj + 2 < J) {
             mid_barrier<4>();
@@ -306,28 +284,20 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
             mid_barrier<0>();
         }
         // ---- second half: kk = 1 MFMAs, next slice's kk = 0 reads, B-half DMA
-        if (stag && iss) dma_b(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa1, fb1, 0, false);
         __builtin_amdgcn_sched_barrier(0);
         if (jj + 1 < J) read_frags(jj + 1, 0, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
-        if (iss) { if (stag) dma_b(jj + 3, 1); else dma_b(jj + 3, 0); }
+        if (iss) dma_b(jj + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
         mfma4(fa1, fb1, 1, false);
         __builtin_amdgcn_sched_barrier(0);
-        if (!stag && iss) dma_b(jj + 3, 1);
+        if (iss) dma_b(jj + 3, 1);
         if (iss) issue_advance();
         __builtin_amdgcn_sched_barrier(0);
 
-        if (kNoEpi && kt == nk - 1) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(acc[m][n][0]));
-            kt = 0;
-            ++ti;
-        } else if (kt == nk - 1) {
+        if (kt == nk - 1) {
             const uint32_t rt = g0 + ti * RG;
             bool stored = false;
             float sc[4] = {1.0f, 1.0f, 1.0f, 1.0f};
@@ -398,26 +368,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                         auto mxv = gm[0] > gm[1] ? gm[0] : gm[1];
                         mxv = mxv > gm[2] ? mxv : gm[2];
                         mxv = mxv > gm[3] ? mxv : gm[3];
-                        if (EPI == 0) {
-                            // (the previous epilogue: per-lane mask over 16 registers)
-                            if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
-                                uint32_t mask = 0;
-#pragma unroll
-                                for (int r = 0; r < 16; ++r)
-                                    mask |= (score(acc[m][n][r], sc[m], n) >= tau[n]) ? (1u << r) : 0u;
-                                while (mask) {
-                                    const int r = __builtin_ctz(mask);
-                                    mask &= mask - 1;
-                                    const uint32_t row = rbase + (r & 3) + 8 * (r >> 2);
-                                    if (row >= p.n_rows) continue;
-                                    auto av = acc[m][n][0];
-#pragma unroll
-                                    for (int rr = 1; rr < 16; ++rr) av = (rr == r) ? acc[m][n][rr] : av;
-                                    emit(score(av, sc[m], n), row);
-                                }
-                                stored = __ballot(stored) != 0;
-                            }
-                        } else if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
+                        if (__ballot(score(mxv, sc[m], n) >= tau[n])) {
                             // hierarchical: only groups whose maximum passes are expanded
 #pragma unroll
                             for (int g = 0; g < 4; ++g) {
@@ -431,10 +382,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                             }
                             stored = __ballot(stored) != 0;
                         }
-                    }
-                    if (EPI == 0 || kNoMath) {  // (EPI >= 1: the next tile's first MFMAs take C = 0)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
                     }
                 }
             }
@@ -455,35 +402,41 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
             if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = ekeys[i];
         }
     }
-    if (STAMP && tid == 0) {
-        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x] = t1 - t0;
-        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x + 1] = r1 - r0;
-    }
 }
 
 // ------------------------------------------------------------------------------------
-// Query-stationary int8 filter (the int8 default when a row is NK = 2..12 slices of 64
-// bytes, i.e. dims up to 768): one workgroup per CU, four waves (one per SIMD, ~420
-// VGPRs each).  Wave w keeps the int8 fragments of its 64 queries (qt*256 + 64w ..) for ALL
-// of K in registers for the workgroup's life, so only corpus rows stream through LDS:
-// 128-row tiles, one 64-byte K slice (8 KiB) per ring slot, 8 slots, 6 slices in flight,
-// one barrier per slice.  Per slice a wave reads 8 KiB of A fragments and issues 16 MFMAs
-// (128 rows x 64 queries x 64 bytes).  Per unit of work that is half the LDS-DMA bytes and
-// two thirds of the LDS-read bytes of k_filter (which re-stages its 256-query B tile for
-// every row tile and reads 192 B of fragments per k per 128x64 wave tile).
-// The K loop is unrolled per tile (the query registers need static indices), so the first
-// MFMAs of a tile take C = 0 without a branch.  Barrier wait: the slice read next has
-// landed for every wave (counted vmcnt: the DMAs of younger slices, and the tile's scale
-// load while it is younger, stay in flight) and this wave's fragment reads are complete.
-// Epilogue as k_filter (EMIT: group-maximum expansion; SAMPLE: scores or maxima to S).
+// Query-stationary int8 filter (the int8 default for rows of an even number of 64-byte
+// slices up to 12, i.e. dims up to 768).
+//
+// One 512-thread workgroup per CU, 8 waves (two per SIMD).  Wave w keeps the int8 B
+// fragments of its 32 queries (qt*256 + 32w ..) for ALL of K in registers for the
+// workgroup's life (96 VGPRs), so only corpus rows move: 128-row tiles stream through an
+// 8-slot LDS ring (one 64-byte K slice = 8 KiB per slot, 6 slices in flight), filled by
+// LDS-DMA (buffer_load ... lds, 1 KiB per wave per slice; the source chunk XOR-swizzled --
+// rows 8..15 of every 16-row group exchange chunks 0<->2, 1<->3 -- so that every
+// ds_read_b128 fragment read below is conflict-free).
+// MFMA shape v_mfma_i32_16x16x64_i8: per slice a wave reads 8 A fragments (16 rows x 64 bytes,
+// one ds_read_b128 each, four row blocks ahead in a 4-register ring) and issues 16 MFMAs
+// (8 row blocks x 2 query blocks of 16).  At the same cycles per op as the 32x32x32 shape it
+// holds a higher clock under load (MI355X_MICROARCH.md, DVFS item 7): measured -12% kernel
+// time at equal work (profiles/r02c_qs16_ab*.txt).
+// Synchronisation: one s_waitcnt vmcnt(N) + s_barrier per two slices, mid-slice (after row
+// block 5 of odd slices): slices <= jj+3 have landed everywhere, with the DMAs of jj+4, jj+5
+// (and the tile's scale load while younger) in flight; the odd slice's DMA follows the
+// barrier, so the slot it refills (slice jj-2's) is free on every wave.  The DMA stream is
+// steady: past the shard's last slice it re-reads the last tile into slots nobody reads
+// again, so every wait is the steady-state count; it drains before the workgroup ends.
+// The first MFMAs of a tile take C = 0 (no accumulator clears).
+// Epilogue (EMIT), in two levels: (1) per query block, the lane's integer maximum over its 32
+// values scored with the tile's largest (for a negative maximum: smallest) 32-row block
+// scale -- never below any of its values' scores -- and one ballot for the whole tile;
+// (2) only if some lane reaches tau: per 16-row block its maximum, then its rows.  Passing
+// (score, row) keys go to a private per-lane LDS ring (CAP entries per query block, entry e
+// of thread t at [e][t], count in a register): no atomics and no waits in the loop; flushed
+// to the per-query global lists at the end or when a block could overfill it.
+// SAMPLE: every tile row is one sampled corpus row; the scores (or one maximum per 32
+// sampled rows) go to S.
 // ------------------------------------------------------------------------------------
-constexpr int kQsRows = 128;               // corpus rows per tile
-constexpr int kQsSlots = 8;                // LDS ring slots
-constexpr int kQsAhead = 6;                // slices issued ahead of the one being consumed
-constexpr int kQsSlot = kQsRows * kSliceB;  // 8 KiB
-constexpr int kQsLaneCap = 20;             // candidate ring entries per (lane, query block)
-
 // s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier for a runtime N in [0, 15] (immediate operand).
 __device__ __forceinline__ void qs_barrier(uint32_t n) {
 #define BSR_QS_WAIT(N) \
@@ -496,71 +449,37 @@ __device__ __forceinline__ void qs_barrier(uint32_t n) {
     }
 #undef BSR_QS_WAIT
 }
-
+// s_waitcnt vmcnt(N) + s_barrier for an N that folds to a constant once the loop is unrolled
 template <int N>
 __device__ __forceinline__ void qs_wait() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
-// qs_wait<n> for an n that folds to a constant once the K loop is unrolled
 __device__ __forceinline__ void qs_wait_n(int n) {
-#define BSR_QS_N(N) \
-    case N: qs_wait<N>(); break;
     switch (n) {
-        BSR_QS_N(1) BSR_QS_N(2) BSR_QS_N(3) BSR_QS_N(4) BSR_QS_N(5) BSR_QS_N(6) BSR_QS_N(7) BSR_QS_N(8)
-        BSR_QS_N(9) BSR_QS_N(10) BSR_QS_N(11) BSR_QS_N(12) BSR_QS_N(13) BSR_QS_N(14) BSR_QS_N(15)
+        case 1: qs_wait<1>(); break;
+        case 2: qs_wait<2>(); break;
+        case 3: qs_wait<3>(); break;
         default: qs_wait<0>(); break;
     }
-#undef BSR_QS_N
 }
 
-// VAR (tooling): 1 = no LDS-DMA in the loop, 5 = no epilogue, 6 = neither.  STAG (tooling):
-// waves 4-7 take each slice's barrier half a slice earlier than their SIMD partners (waves
-// 0-3).
-template <bool EMIT, int NK, int NB, bool STAMP, int VAR = 0, bool STAG = false>
-__device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
-    // VAR + 8 (P - 1): one barrier per P slices (P = 2: 8-slot ring, 6 slices ahead; P = 3:
-    // 10 slots, 7 ahead; P = 3 falls back to 2 when it does not divide NK).  See the loop.
-    constexpr int kV = VAR & 7, kPr = ((VAR >> 3) & 7) + 1, kP = (NK % kPr == 0) ? kPr : 2;
-    // VAR + 64 (P > 1 only): steady DMA stream -- the DMAs never stop early (slices past the
-    // end re-read the last tile into slots nobody reads again), so every wait is the
-    // steady-state count and hipcc sees the same number of VMEM ops on every path (its own
-    // wait for the tile's scale load is then not a full drain).  Drained before exit.
-    constexpr bool kSteady = (VAR & 64) != 0 && kPr >= 2;
-    constexpr bool kNoDMA = kV == 1 || kV == 6, kNoEpi = kV == 5 || kV == 6, kB2 = kPr >= 2;
-    // VAR + 128 (P = 2, tooling): a 9-slot ring with 7 slices ahead (one more DMA in flight)
-    constexpr bool kDeep = (VAR & 128) != 0 && kP == 2;
-    constexpr int kS = kP == 3 ? 10 : (kDeep ? 9 : kQsSlots), kA = kP == 3 ? 7 : (kDeep ? 7 : kQsAhead);
-    static_assert(!kB2 || (kS >= kA + kP && kA >= kP + 2), "ring: slot reuse and landing margins");
-    // NB query blocks of 32 per wave: NB = 2 -> 4 waves x 64 queries (one wave per SIMD);
-    // NB = 1 -> 8 waves x 32 queries (two per SIMD, 96 query registers each)
-    constexpr int NT = 64 * (8 / NB), QW = 32 * NB;
-    uint64_t t0 = 0, r0 = 0, c_bar = 0, c_dma = 0, c_epi = 0;
-    if (STAMP) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-    // (STAMP: per-segment cycle counters of wave 0 -- barrier waits, DMA issue, epilogue)
-    auto stamp = [&]() -> uint64_t {
-        uint64_t t;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return t;
-    };
+typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
+
+__device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
+
+template <bool EMIT, int NK>
+__global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
+    constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
+    constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
+    constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
-    constexpr int BM = kQsRows, BN = kFilterTile;
-    // LDS: the ring; then (EMIT) a private candidate ring of kQsLaneCap keys per (lane, query
-    // block), entry e of thread t at [e][t] (conflict-free), its count in a register: no
-    // atomics and no waits in the epilogue, the rings go to the per-query global lists once,
-    // at the end (earlier if a block's rows could overfill it).
-    constexpr int EM_BYTES = EMIT ? NT * NB * kQsLaneCap * 8 : 0;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[kS * kQsSlot + EM_BYTES];
+    constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds + kS * kQsSlot) + tid;
-    uint32_t ecnt[NB];
-#pragma unroll
-    for (int n = 0; n < NB; ++n) ecnt[n] = 0;
+    uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
+    uint32_t ecnt[2] = {0, 0};
 
-    // Grid as k_filter: per XCD, G row groups x n_qt query tiles; a row tile's readers share
-    // the XCD's L2.
     const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const uint32_t G = (gridDim.x >> 3) / p.n_qt;
     const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
@@ -571,285 +490,198 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
     const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
     const uint32_t J = my_rt * NK;
 
-    // The wave's query fragments, all K: fb[n][s] = queries .. + n*32 + (lane & 31),
-    // bytes 32s + 16(lane >> 5) .. +15 (the MFMA B layout).
-    i32x4_t fb[NB][2 * NK];
+    // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
+    // qt*256 + 32w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
+    uint32_t qq[2];
+    i32x4v_t fb[2][NK];
+    float tau[2], sbq[2];
 #pragma unroll
-    for (int n = 0; n < NB; ++n) {
-        const uint8_t* src = p.B + (uint64_t)(qt * BN + w * QW + n * 32 + (lane & 31)) * p.row_bytes + 16 * (lane >> 5);
+    for (int nb = 0; nb < 2; ++nb) {
+        qq[nb] = qt * BN + w * 32 + nb * 16 + (lane & 15);
+        const uint8_t* src = p.B + (uint64_t)qq[nb] * p.row_bytes + 16 * (lane >> 4);
 #pragma unroll
-        for (int s2 = 0; s2 < 2 * NK; ++s2) fb[n][s2] = *reinterpret_cast<const i32x4_t*>(src + 32 * s2);
+        for (int kt = 0; kt < NK; ++kt) fb[nb][kt] = *reinterpret_cast<const i32x4v_t*>(src + 64 * kt);
+        tau[nb] = EMIT ? p.tau[qq[nb]] : 0.0f;
+        sbq[nb] = p.b_scale[qq[nb]];
     }
-    float tau[NB], sbq[NB];
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-        const uint32_t q = qt * BN + w * QW + n * 32 + (lane & 31);
-        tau[n] = 0.0f;
-        if (EMIT) tau[n] = p.tau[q];
-        sbq[n] = p.b_scale[q];
-    }
-    // the lane's ring of query block n to the query's global list (a count past cap marks the
-    // list overflowed: not certified from it)
-    auto flush_ring = [&](int n) {
-        const uint32_t q = qt * BN + w * QW + n * 32 + (lane & 31), nn = ecnt[n];
+    auto flush_ring = [&](int nb) {
+        const uint32_t nn = ecnt[nb];
         if (nn) {
-            const uint32_t gp = atomicAdd(p.cnt + q, nn);
+            const uint32_t gp = atomicAdd(p.cnt + qq[nb], nn);
             for (uint32_t i = 0; i < nn; ++i)
-                if (gp + i < p.cap) p.cand[(uint64_t)q * p.cap + gp + i] = lkeys[(n * kQsLaneCap + i) * NT];
+                if (gp + i < p.cap) p.cand[(uint64_t)qq[nb] * p.cap + gp + i] = lkeys[(nb * CAP + i) * NT];
         }
-        ecnt[n] = 0;
+        ecnt[nb] = 0;
     };
 
-    // LDS-DMA: wave w fills rows (NB*w+i)*16 .. +15 of each slice (1 KiB per instruction),
-    // XOR-swizzled on the source chunk as k_filter.
-    uint32_t lrow[NB], aoff_dma[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        lrow[i] = (w * NB + i) * 16 + (lane >> 2);
-        aoff_dma[i] = lrow[i] * (uint32_t)p.a_stride + (((lane & 3) ^ ((lrow[i] >> 2) & 3)) * 16);
-    }
+    // LDS-DMA: wave w fills rows 16w .. 16w+15 of each slice (1 KiB per instruction); the
+    // source chunk is XOR-swizzled so that LDS chunk position p holds global chunk p ^ swz.
+    const uint32_t lrow = w * 16 + (lane >> 2);
+    const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
+    uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
     uint32_t iss_ti = 0, iss_kt = 0;
     __amdgpu_buffer_rsrc_t rsrc_a;
     auto set_issue_tile = [&]() {
         const uint32_t rt = g0 + iss_ti * RG;
         rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
                                                    BM * (uint32_t)p.a_stride, 0x00020000);
-        if (!EMIT) {  // sample pass: tail rows read the last valid row
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const uint32_t r = rt * BM + lrow[i] < p.n_rows ? lrow[i] : p.n_rows - 1 - rt * BM;
-                aoff_dma[i] = r * (uint32_t)p.a_stride + (((lane & 3) ^ ((lrow[i] >> 2) & 3)) * 16);
-            }
+        if (!EMIT) {
+            const uint32_t r = rt * BM + lrow < p.n_rows ? lrow : p.n_rows - 1 - rt * BM;
+            aoff_dma = r * (uint32_t)p.a_stride + lchunk;
         }
     };
-    // DMA i (< NB) of slice jj = (iss_ti, iss_kt); the last advances the issue state
-    auto issue_dma = [&](uint32_t jj, int i) {
-        uint8_t* la = lds + (jj % kS) * kQsSlot + wu * (NB * 1024) + i * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma[i], iss_kt * kSliceB, 0, 0);
-        if (i == NB - 1 && ++iss_kt == NK) {
+    auto issue_dma = [&](uint32_t jj) {
+        uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma, iss_kt * kSliceB, 0, 0);
+        if (++iss_kt == NK) {
             iss_kt = 0;
             ++iss_ti;
             if (iss_ti < my_rt) set_issue_tile();
         }
     };
-
-    int aoff[4][2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int row = m * 32 + (lane & 31);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int lc = 2 * kk + (lane >> 5);
-            aoff[m][kk] = row * kSliceB + ((lc ^ ((row >> 2) & 3)) * 16);
-        }
-    }
-    // A fragments [m][kk]; fa[.][kk] of the next slice are read as soon as this slice's kk
-    // MFMAs have issued (one register set: the query fragments fill most of the file)
-    i32x4_t fa[4][2];
-    auto read_frag = [&](uint32_t jj, int m, int kk) {
-        fa[m][kk] = *reinterpret_cast<const i32x4_t*>(lds + (jj % kS) * kQsSlot + aoff[m][kk]);
+    // A fragment of row block rb (rows 16rb .. +15): lane -> row 16rb + (lane & 15), chunk
+    // lane >> 4; the swizzle depends on row & 15 only, so block rb is at a constant 1 KiB step
+    const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
+    // four fragment registers, read four row blocks ahead: block rb of slice jj lands in
+    // fa[rb & 3] while the MFMAs of block rb - 4 (the same slice, or the previous one) run
+    i32x4v_t fa[4];
+    auto read_frag = [&](uint32_t jj, int rb) {
+        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
     };
 
-    i32x16_t acc[4][NB];
-    // Prologue: slices 0..min(J, kQsAhead)-1 issued; slice 0 landed everywhere; its
-    // fragments read.
+    i32x4v_t acc[8][2];
     if (my_rt) set_issue_tile();
-    const uint32_t pre = kSteady ? (J ? (uint32_t)kA : 0u) : (J < (uint32_t)kA ? J : (uint32_t)kA);
-    for (uint32_t jj = 0; jj < pre; ++jj)
-#pragma unroll
-        for (int i = 0; i < NB; ++i) issue_dma(jj, i);
-    // slices 0 and 1 (B2: 0, 1 and 2) landed everywhere
-    if (kB2) qs_barrier(pre >= kP + 1 ? NB * (pre - kP - 1) : 0);
-    else qs_barrier(pre >= 2 ? NB * (pre - 2) : 0);
+    const uint32_t pre = J ? (uint32_t)A : 0u;
+    for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
+    qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
     if (J)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) { read_frag(0, m, 0); read_frag(0, m, 1); }
+        for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
 
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
-        // the tile's block scales: a plain load (hipcc drains vmcnt(0) at its use in the
-        // epilogue; an LDS-DMA of the scales, which avoids that drain, measured 5% slower)
         float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
 #pragma unroll
         for (int kt = 0; kt < NK; ++kt) {
             const uint32_t jj = t * NK + kt;
-            // Per K half, per m: the two MFMAs of A block m, then the next slice's fragment
-            // of block m (landed: previous barrier; the register is free once both MFMAs
-            // issued).  The DMAs of slice jj + kQsAhead and the barrier sit between MFMA
-            // pairs, so one wave per SIMD keeps its MFMA pipe fed while they issue.
+            const bool bar_slice = (kt & 1) == 1;
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
+            for (int rb = 0; rb < 8; ++rb) {
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-#pragma unroll
-                    for (int n = 0; n < NB; ++n) {
-                        if (kt == 0 && kk == 0) {
-                            const i32x16_t z = {};
-                            acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m][kk], fb[n][2 * kt + kk], z, 0, 0, 0);
-                        } else {
-                            acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m][kk], fb[n][2 * kt + kk], acc[m][n], 0, 0, 0);
-                        }
+                for (int nb = 0; nb < 2; ++nb) {
+                    if (kt == 0) {
+                        const i32x4v_t z = {};
+                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], z, 0, 0, 0);
+                    } else {
+                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], acc[rb][nb], 0, 0, 0);
                     }
-                    __builtin_amdgcn_sched_barrier(0);
-                    read_frag(jj + 1, m, kk);  // (past the stream's end: unused; unconditional
-                                               // so hipcc can count the LDS reads exactly)
-                    // B2, odd slices: the DMAs follow the slice's barrier (the slot they refill,
-                    // slice jj - 2's, is free once every wave is past it)
-                    const bool kBarSlice = kB2 && (kt % kP) == kP - 1;
-                    const bool dma_here = kBarSlice ? (kk == 1 && m >= 2 && m - 2 < NB)
-                                                             : (kk == 0 && (m & 1) && (m >> 1) < NB);
-                    if (!kNoDMA && dma_here && (kSteady || jj + kA < J)) {
-                        uint64_t ts = 0;
-                        if (STAMP) ts = stamp();
-                        issue_dma(jj + kA, kBarSlice ? m - 2 : m >> 1);
-                        if (STAMP) c_dma += stamp() - ts;
-                    }
-                    // Barrier: the slice after next has landed everywhere.  Younger VMEM ops
-                    // stay in flight: the DMAs of slices jj+3 .. jj+kQsAhead (NB each) and,
-                    // while it is younger than slice jj+2 (kt <= 3), the tile's scale load.
-                    // No lgkmcnt: the slot a DMA refills next step was read two steps ago
-                    // (hipcc waited for those reads before their MFMAs).
-                    // P > 1: a barrier on every P-th slice only, once slices up to jj + P + 1
-                    // have landed everywhere (the reads before the next barrier, P slices on,
-                    // reach slice jj + P + 1); in flight: the DMAs of slices jj + P + 2 ..
-                    // jj + A - 1 (this slice's DMA follows the barrier) and, while younger than
-                    // slice jj + P + 1 (kt <= A - P - 2), the tile's scale load.  A DMA refills
-                    // slice jj + A - S's slot: every wave is past it (S >= A + P).
-                    if (kBarSlice && m == 1 && kk == 1) {
-                        uint64_t tb = 0;
-                        if (STAMP) tb = stamp();
-                        const int kSc = (EMIT && kt <= kA - kP - 2) ? 1 : 0;
-                        if (kSteady ? jj + 1 < J : jj + kA < J) {
-                            qs_wait_n(NB * (kA - kP - 2) + kSc);
-                        } else if (jj + 1 < J) {
-                            const uint32_t last = J - 1;  // every DMA issued
-                            qs_barrier((last > jj + kP + 1 ? NB * (last - jj - kP - 1) : 0) + kSc);
-                        }
-                        if (STAMP) c_bar += stamp() - tb;
-                    }
-                    if (!kB2 && m == 1 && kk == ((STAG && wu >= 4) ? 0 : 1)) {
-                        uint64_t tb = 0;
-                        if (STAMP) tb = stamp();
-                        if (jj + kA < J) {
-                            qs_wait_n(NB * (kA - 2) + ((EMIT && kt <= 3) ? 1 : 0));  // (folds: kt unrolled)
-                        } else if (jj + 1 < J) {  // the stream's last slices, counted at run time
-                            qs_barrier((J - 1 > jj + 2 ? NB * (J - 1 - jj - 2) : 0) + ((EMIT && kt <= 3) ? 1 : 0));
-                        }
-                        if (STAMP) c_bar += stamp() - tb;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
                 }
+                __builtin_amdgcn_sched_barrier(0);
+                if (rb < 4) read_frag(jj, rb + 4);
+                else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
+                // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
+                // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
+                if (bar_slice ? rb == 6 : rb == 1) issue_dma(jj + A);
+                // barrier (odd slices, after group 5): slices <= jj + 3 landed everywhere (the
+                // reads before the next barrier reach rows 0-1 of slice jj + 3); in flight: the
+                // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
+                // the tile's scale load
+                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if constexpr (kNoEpi) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < NB; ++n) asm volatile("" ::"v"(acc[m][n][0]));
-            continue;
-        }
-        // ---- epilogue (VAR + 256, tooling: at raised wave priority)
-        if constexpr ((VAR & 256) != 0) __builtin_amdgcn_s_setprio(2);
-        uint64_t te = 0;
-        if (STAMP) te = stamp();
-        bool stored = false;
+        // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
         const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
+        bool stored = false;
+        if constexpr (!EMIT) {
+            // sample pass: tile row r is corpus row 32r (a_row_mult == kQuantBlock), whose scale
+            // is a_scale[r]; tail rows (re-reads of the last sampled row) take its scale too
+            const float sc_last = p.a_scale[p.n_rows - 1];
+            float pmax[2] = {0.0f, 0.0f};  // compact: the even row block's maxima
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+            for (int rb = 0; rb < 8; ++rb) {
+                const uint32_t rbase = rt * BM + rb * 16 + 4 * (lane >> 4);
+                const float4 s4 = *reinterpret_cast<const float4*>(p.a_scale + rbase);
+                const float srow4[4] = {rbase < p.n_rows ? s4.x : sc_last, rbase + 1 < p.n_rows ? s4.y : sc_last,
+                                        rbase + 2 < p.n_rows ? s4.z : sc_last, rbase + 3 < p.n_rows ? s4.w : sc_last};
 #pragma unroll
-            for (int n = 0; n < NB; ++n) {
-                const uint32_t ql = w * QW + n * 32 + (lane & 31);
-                const uint32_t rbase = rt * BM + m * 32 + 4 * (lane >> 5);
-                auto score = [&](int v, float s_r) -> float { return ((float)v * s_r) * sbq[n]; };
-                if constexpr (!EMIT) {
-                    float v[16];
+                for (int nb = 0; nb < 2; ++nb) {
+                    float v[4];
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
-                        tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                        v[r] = score(acc[m][n][r], p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]);
-                    }
-                    float* srow = p.S + (uint64_t)(qt * BN + ql) * p.s_ld;
+                    for (int r = 0; r < 4; ++r) v[r] = ((float)acc[rb][nb][r] * srow4[r]) * sbq[nb];
+                    float* srow = p.S + (uint64_t)qq[nb] * p.s_ld;
                     if (!p.s_compact) {
-#pragma unroll
-                        for (int g = 0; g < 4; ++g)
-                            *reinterpret_cast<float4*>(srow + rbase + 8 * g) =
-                                make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+                        *reinterpret_cast<float4*>(srow + rbase) = make_float4(v[0], v[1], v[2], v[3]);
                     } else {
-                        float mx = v[0];
-#pragma unroll
-                        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, v[r]);
+                        float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+                        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
                         mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-                        if (lane < 32) srow[(rt * BM + m * 32) / 32] = mx;
+                        if (rb & 1) {
+                            mx = fmaxf(mx, pmax[nb]);
+                            if (lane < 16) srow[(rt * BM + (rb - 1) * 16) / 32] = mx;
+                        } else {
+                            pmax[nb] = mx;
+                        }
                     }
-                    stored = true;
-                } else {
-                    auto emit = [&](float v, uint32_t row) {
-                        lkeys[(n * kQsLaneCap + ecnt[n]) * NT] = score_key(v, row);
-                        ++ecnt[n];
-                    };
-                    int gm[4];
+                }
+            }
+            stored = true;
+        } else {
+            // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
+            // each query block, scored with the tile's largest (or, for a negative maximum,
+            // smallest) block scale -- never below any of its values' scores
+            const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+            const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
+            bool any = false;
+            int mrb[2];  // (unused lanes' values are never read)
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int x = max(acc[m][n][4 * g], acc[m][n][4 * g + 1]);
-                        const int y = max(acc[m][n][4 * g + 2], acc[m][n][4 * g + 3]);
-                        gm[g] = max(x, y);
-                    }
-                    const int mxv = max(max(gm[0], gm[1]), max(gm[2], gm[3]));
-                    if (__ballot(score(mxv, sc[m]) >= tau[n])) {
-                        // room for this block's up to 16 rows in every lane's ring (rarely
-                        // not: dense emission, e.g. large k)
-                        if (__ballot(ecnt[n] > (uint32_t)(kQsLaneCap - 16))) flush_ring(n);
-                        // only the groups whose maximum passes are expanded; each register
-                        // appends under its own lane mask
+            for (int nb = 0; nb < 2; ++nb) {
+                int m = acc[0][nb][0];
 #pragma unroll
-                        for (int g = 0; g < 4; ++g) {
-                            if (!__ballot(score(gm[g], sc[m]) >= tau[n])) continue;
+                for (int rb = 0; rb < 8; ++rb)
 #pragma unroll
-                            for (int i = 0; i < 4; ++i) {
-                                const float v = score(acc[m][n][4 * g + i], sc[m]);
-                                const uint32_t row = rbase + 8 * g + i;
-                                if (v >= tau[n] && row < p.n_rows) emit(v, row);
+                    for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m;
+                mrb[nb] = m;
+                any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
+            }
+            if (__ballot(any)) {
+                // level 2: per (query block, 16-row block): its maximum, then its rows
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
+#pragma unroll
+                    for (int rb = 0; rb < 8; ++rb) {
+                        const i32x4v_t& x = acc[rb][nb];
+                        const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
+                        const float scr = sc[rb >> 1];
+                        if (!__ballot(((float)bm * scr) * sbq[nb] >= tau[nb])) continue;
+                        if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
+                            flush_ring(nb);
+                            stored = true;
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float v = ((float)x[r] * scr) * sbq[nb];
+                            const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
+                            if (v >= tau[nb] && row < p.n_rows) {
+                                lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
+                                ++ecnt[nb];
                             }
                         }
                     }
                 }
             }
         }
-        // global stores / atomics count in vmcnt: drain them so the counted waits stay exact
-        if (stored) wait_vm0();
-        if constexpr ((VAR & 256) != 0) __builtin_amdgcn_s_setprio(0);
-        if (STAMP) c_epi += stamp() - te;
+        if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
     }
-    if (kSteady) wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
+    wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
     if constexpr (EMIT) {
-#pragma unroll
-        for (int n = 0; n < NB; ++n) flush_ring(n);
-    }
-    if (STAMP && tid == 0) {
-        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x] = t1 - t0;
-        reinterpret_cast<uint64_t*>(p.S)[2 * blockIdx.x + 1] = r1 - r0;
-        uint64_t* seg = reinterpret_cast<uint64_t*>(p.S) + 2 * gridDim.x + 4 * blockIdx.x;
-        seg[0] = c_bar;
-        seg[1] = c_dma;
-        seg[2] = c_epi;
-        seg[3] = J;
+        flush_ring(0);
+        flush_ring(1);
     }
 }
 
-// One wave per SIMD (NB = 2) and two per SIMD (NB = 1): separate kernels, so each gets
-// its register budget from a plain __launch_bounds__.
-template <bool EMIT, int NK, int NB = 2, bool STAMP = false>
-__global__ __launch_bounds__(256, 1) void k_filter_qs(GemmArgs p) {
-    static_assert(NB == 2, "k_filter_qs: 4 waves x 64 queries");
-    filter_qs_body<EMIT, NK, 2, STAMP>(p);
-}
-template <bool EMIT, int NK, bool STAMP = false, int VAR = 0, bool STAG = false>
-__global__ __launch_bounds__(512, 1) void k_filter_qs8(GemmArgs p) {
-    filter_qs_body<EMIT, NK, 1, STAMP, VAR, STAG>(p);
-}
 
 // ------------------------------------------------------------------------------------
 // Skinny int8 filter for batches of at most 16 queries (single-query latency path): the
@@ -1181,26 +1013,20 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
     return hipGetLastError();
 }
 
-// product variant of the query-stationary kernel: 8 = one barrier per two slices (B2;
-// -5% kernel time vs one per slice, profiles/r01l_*), + 64 = steady DMA stream (no full
-// vmcnt drain at each tile's epilogue; -1.5%, profiles/r01n_*).  A/B builds override it
-// (tools/ab).
-#ifndef BSR_QS_VAR
-#define BSR_QS_VAR 72
-#endif
-// int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
-// query-stationary kernel; other int8 widths and bf16: k_filter.
+// int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the query-stationary
+// kernel; other int8 widths and the bf16 operand: k_filter.
 template <bool EMIT>
 static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
     if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
+        const dim3 g(grid), b(512);
         switch (nk) {
-            case 2: BSR_KLAUNCH((k_filter_qs8<EMIT, 2, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 4: BSR_KLAUNCH((k_filter_qs8<EMIT, 4, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 6: BSR_KLAUNCH((k_filter_qs8<EMIT, 6, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 8: BSR_KLAUNCH((k_filter_qs8<EMIT, 8, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 10: BSR_KLAUNCH((k_filter_qs8<EMIT, 10, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            default: BSR_KLAUNCH((k_filter_qs8<EMIT, 12, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
+            case 2: BSR_KLAUNCH((k_filter_qs16<EMIT, 2>), g, b, s, e0, e1, a); return;
+            case 4: BSR_KLAUNCH((k_filter_qs16<EMIT, 4>), g, b, s, e0, e1, a); return;
+            case 6: BSR_KLAUNCH((k_filter_qs16<EMIT, 6>), g, b, s, e0, e1, a); return;
+            case 8: BSR_KLAUNCH((k_filter_qs16<EMIT, 8>), g, b, s, e0, e1, a); return;
+            case 10: BSR_KLAUNCH((k_filter_qs16<EMIT, 10>), g, b, s, e0, e1, a); return;
+            default: BSR_KLAUNCH((k_filter_qs16<EMIT, 12>), g, b, s, e0, e1, a); return;
         }
     }
     if (op == kFilterI8)

@@ -13,6 +13,7 @@ constexpr uint32_t kRowPad = 256;      // rows are padded to a multiple of this 
 constexpr uint32_t kScanQF = 8;        // queries per exact-scan launch (max)
 constexpr uint32_t kSampleStride = 32; // candidate-threshold sample: every 32nd row
 constexpr uint32_t kQuantBlock = 32;   // rows sharing one int8 scale (one 32-row MFMA block)
+static_assert(kSampleStride == kQuantBlock, "sample pass: sampled row r has scale a_scale[r]");
 constexpr uint32_t kFilterTile = 256;  // MFMA filter tile: 256 corpus rows x 256 queries
 
 // Operand type of the MFMA candidate filter.

@@ -9,6 +9,7 @@
 #include <string.h>
 
 using namespace bsr;
+using namespace bsrlab;
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 // bf16: U(-0.036, 0.036) per element; int8: U{-127..127} (scores = I * s_a * s_b)

@@ -1141,113 +1141,4 @@ __global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__
     }
 }
 
-// ------------------------------------------------------------------------------------
-// Launchers
-// ------------------------------------------------------------------------------------
-// Workgroups for the persistent filter: 8 XCDs x (32 CUs rounded down to a multiple of n_qt).
-static uint32_t filter_grid(uint32_t n_qt) {
-    const uint32_t per_xcd = n_qt >= 32 ? n_qt : (32 / n_qt) * n_qt;
-    return 8 * per_xcd;
-}
-
-// Filter launches: with timing events, hipExtLaunchKernel records them at the kernel's own
-// dispatch and completion; without, a plain launch (also inside stream capture).
-#define BSR_KLAUNCH(K, G, B, S, E0, E1, A)                               \
-    do {                                                                 \
-        if (E0) hipExtLaunchKernelGGL(K, G, B, 0, S, E0, E1, 0u, A);     \
-        else hipLaunchKernelGGL(K, G, B, 0, S, A);                       \
-    } while (0)
-
-static uint32_t skinny_grid(uint32_t n_rows) {
-    const uint32_t groups = (n_rows + 31) / 32, wgs = (groups + 3) / 4;
-    return wgs < 768 ? (wgs ? wgs : 1) : 768;  // 3 workgroups per CU (VGPR-limited occupancy)
-}
-// v2 for rows of <= 16 K steps (1024 int8), v1 beyond.
-template <bool EMIT>
-static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const uint32_t nk = a.row_bytes / kSliceB;
-    // v2 holds ~170 VGPRs: 2 waves per SIMD = 2 workgroups per CU
-    const uint32_t units = (a.n_rows + 15) / 16, g2 = std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
-    const dim3 g(nk <= 16 ? g2 : skinny_grid(a.n_rows)), b(256);
-    if (nk <= 4) BSR_KLAUNCH((k_filter_skinny2<EMIT, 4>), g, b, s, e0, e1, a);
-    else if (nk <= 8) BSR_KLAUNCH((k_filter_skinny2<EMIT, 8>), g, b, s, e0, e1, a);
-    else if (nk <= 12) BSR_KLAUNCH((k_filter_skinny2<EMIT, 12>), g, b, s, e0, e1, a);
-    else if (nk <= 16) BSR_KLAUNCH((k_filter_skinny2<EMIT, 16>), g, b, s, e0, e1, a);
-    else BSR_KLAUNCH(k_filter_skinny<EMIT>, g, b, s, e0, e1, a);
-}
-hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_skinny<false>(a, s, e0, e1);
-    return hipGetLastError();
-}
-hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_skinny<true>(a, s, e0, e1);
-    return hipGetLastError();
-}
-
-// product variant of the query-stationary kernel: 8 = one barrier per two slices (B2;
-// -5% kernel time vs one per slice, profiles/r01l_*), + 64 = steady DMA stream (no full
-// vmcnt drain at each tile's epilogue; -1.5%, profiles/r01n_*).  A/B builds override it
-// (tools/ab).
-#ifndef BSR_QS_VAR
-#define BSR_QS_VAR 72
-#endif
-// int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the
-// query-stationary kernel; other int8 widths and bf16: k_filter.
-template <bool EMIT>
-static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
-    if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
-        switch (nk) {
-            case 2: BSR_KLAUNCH((k_filter_qs8<EMIT, 2, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 4: BSR_KLAUNCH((k_filter_qs8<EMIT, 4, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 6: BSR_KLAUNCH((k_filter_qs8<EMIT, 6, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 8: BSR_KLAUNCH((k_filter_qs8<EMIT, 8, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            case 10: BSR_KLAUNCH((k_filter_qs8<EMIT, 10, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-            default: BSR_KLAUNCH((k_filter_qs8<EMIT, 12, false, BSR_QS_VAR>), dim3(grid), dim3(512), s, e0, e1, a); return;
-        }
-    }
-    if (op == kFilterI8)
-        BSR_KLAUNCH((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
-    else
-        BSR_KLAUNCH((k_filter<OpBF16, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
-}
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_filter<false>(op, a, s, e0, e1);
-    return hipGetLastError();
-}
-hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_filter<true>(op, a, s, e0, e1);
-    return hipGetLastError();
-}
-hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,
-                             const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(k_select_tau, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau, cnt,
-                       status);
-    return hipGetLastError();
-}
-hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,
-                              const float* tau, uint32_t kp, uint32_t* cand_rows, uint32_t* ncand,
-                              float* tau_excl, uint32_t* status, hipStream_t s) {
-    const uint32_t e = (kp + 1 + 63) / 64;
-#define BSR_SELECT(E)                                                                                   \
-    hipLaunchKernelGGL(k_select_cand<E>, dim3(nq), dim3(64), 0, s, cand, cnt, cap, nq, tau, kp, cand_rows, \
-                       ncand, tau_excl, status)
-    switch (e) {
-        case 1: BSR_SELECT(1); break;
-        case 2: BSR_SELECT(2); break;
-        case 3: BSR_SELECT(3); break;
-        case 4: BSR_SELECT(4); break;
-        case 5: BSR_SELECT(5); break;
-        case 6: BSR_SELECT(6); break;
-        case 7: BSR_SELECT(7); break;
-        case 8: BSR_SELECT(8); break;
-        case 9: BSR_SELECT(9); break;
-        case 10: BSR_SELECT(10); break;
-        default: return hipErrorInvalidValue;
-    }
-#undef BSR_SELECT
-    return hipGetLastError();
-}
-
 }  // namespace bsrlab

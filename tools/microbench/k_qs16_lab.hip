@@ -1,0 +1,238 @@
+// k_qs16_lab.hip -- TOOLING (candidate for the product): the query-stationary int8 filter of
+// round 1 (k_filter_qs8: 8 waves, 32 queries per wave in registers, 128-row tiles through an
+// 8-slot LDS ring, one s_barrier per two slices, steady LDS-DMA stream) with the
+// v_mfma_i32_16x16x64_i8 shape instead of v_mfma_i32_32x32x32_i8 (MI355X_MICROARCH.md,
+// DVFS item 7: the 16x16 shape holds a higher clock at about equal cycles per op).
+// Per slice a wave reads 8 A fragments (16 rows x 64 bytes each, one ds_read_b128) and issues
+// 16 MFMAs (8 row blocks x 2 query blocks of 16).  LDS chunk swizzle for the 16-row read
+// pattern: rows 8..15 of every 16-row group XOR their chunk with 2 (conflict-free for the
+// four ds_read_b128 lane groups).
+// Included after the product k_filter.hip (uses its types and helpers).
+namespace bsrlab {
+using namespace bsr;
+
+typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
+
+__device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
+
+// VAR bits (tooling): 1 no DMA, 2 no epilogue
+template <bool EMIT, int NK, int VAR = 0>
+__global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
+    constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
+    constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
+    constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
+    constexpr bool kNoDMA = VAR & 1, kNoEpi = VAR & 2;
+    static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
+    constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
+    uint32_t ecnt[2] = {0, 0};
+
+    const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const uint32_t G = (gridDim.x >> 3) / p.n_qt;
+    const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
+    const bool active = slot < G * p.n_qt;
+    const uint32_t qt = active ? slot % p.n_qt : 0;
+    const uint32_t g0 = xcd * G + (active ? slot / p.n_qt : 0);
+    const uint32_t RG = 8 * G;
+    const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
+    const uint32_t J = my_rt * NK;
+
+    // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
+    // qt*256 + 32w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
+    uint32_t qq[2];
+    i32x4v_t fb[2][NK];
+    float tau[2], sbq[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        qq[nb] = qt * BN + w * 32 + nb * 16 + (lane & 15);
+        const uint8_t* src = p.B + (uint64_t)qq[nb] * p.row_bytes + 16 * (lane >> 4);
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) fb[nb][kt] = *reinterpret_cast<const i32x4v_t*>(src + 64 * kt);
+        tau[nb] = EMIT ? p.tau[qq[nb]] : 0.0f;
+        sbq[nb] = p.b_scale[qq[nb]];
+    }
+    auto flush_ring = [&](int nb) {
+        const uint32_t nn = ecnt[nb];
+        if (nn) {
+            const uint32_t gp = atomicAdd(p.cnt + qq[nb], nn);
+            for (uint32_t i = 0; i < nn; ++i)
+                if (gp + i < p.cap) p.cand[(uint64_t)qq[nb] * p.cap + gp + i] = lkeys[(nb * CAP + i) * NT];
+        }
+        ecnt[nb] = 0;
+    };
+
+    // LDS-DMA: wave w fills rows 16w .. 16w+15 of each slice (1 KiB per instruction); the
+    // source chunk is XOR-swizzled so that LDS chunk position p holds global chunk p ^ swz.
+    const uint32_t lrow = w * 16 + (lane >> 2);
+    const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
+    uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
+    uint32_t iss_ti = 0, iss_kt = 0;
+    __amdgpu_buffer_rsrc_t rsrc_a;
+    auto set_issue_tile = [&]() {
+        const uint32_t rt = g0 + iss_ti * RG;
+        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
+                                                   BM * (uint32_t)p.a_stride, 0x00020000);
+        if (!EMIT) {
+            const uint32_t r = rt * BM + lrow < p.n_rows ? lrow : p.n_rows - 1 - rt * BM;
+            aoff_dma = r * (uint32_t)p.a_stride + lchunk;
+        }
+    };
+    auto issue_dma = [&](uint32_t jj) {
+        uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma, iss_kt * kSliceB, 0, 0);
+        if (++iss_kt == NK) {
+            iss_kt = 0;
+            ++iss_ti;
+            if (iss_ti < my_rt) set_issue_tile();
+        }
+    };
+    // A fragment of row block rb (rows 16rb .. +15): lane -> row 16rb + (lane & 15), chunk
+    // lane >> 4; the swizzle depends on row & 15 only, so block rb is at a constant 1 KiB step
+    const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
+    // four fragment registers, read four row blocks ahead: block rb of slice jj lands in
+    // fa[rb & 3] while the MFMAs of block rb - 4 (the same slice, or the previous one) run
+    i32x4v_t fa[4];
+    auto read_frag = [&](uint32_t jj, int rb) {
+        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (kNoDMA ? 0 : jj % S) * SLOT + rb * 1024 + aoff0);
+    };
+
+    i32x4v_t acc[8][2];
+    if (my_rt) set_issue_tile();
+    const uint32_t pre = J ? (uint32_t)A : 0u;
+    for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
+    qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
+    if (J)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
+
+    for (uint32_t t = 0; t < my_rt; ++t) {
+        const uint32_t rt = g0 + t * RG;
+        float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) {
+            const uint32_t jj = t * NK + kt;
+            const bool bar_slice = (kt & 1) == 1;
+#pragma unroll
+            for (int rb = 0; rb < 8; ++rb) {
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    if (kt == 0) {
+                        const i32x4v_t z = {};
+                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], z, 0, 0, 0);
+                    } else {
+                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], acc[rb][nb], 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (rb < 4) read_frag(jj, rb + 4);
+                else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
+                // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
+                // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
+                if (!kNoDMA && (bar_slice ? rb == 6 : rb == 1)) issue_dma(jj + A);
+                // barrier (odd slices, after group 5): slices <= jj + 3 landed everywhere (the
+                // reads before the next barrier reach rows 0-1 of slice jj + 3); in flight: the
+                // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
+                // the tile's scale load
+                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (kNoEpi) {
+#pragma unroll
+            for (int rb = 0; rb < 8; ++rb) asm volatile("" ::"v"(acc[rb][0]), "v"(acc[rb][1]));
+            continue;
+        }
+        // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
+        const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
+        bool stored = false;
+        if constexpr (!EMIT) {
+            float pmax[2] = {0.0f, 0.0f};  // compact: the even row block's maxima
+#pragma unroll
+            for (int rb = 0; rb < 8; ++rb) {
+                const uint32_t rbase = rt * BM + rb * 16 + 4 * (lane >> 4);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        uint32_t tr = rbase + r;
+                        tr = tr < p.n_rows ? tr : p.n_rows - 1;
+                        v[r] = ((float)acc[rb][nb][r] * p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]) * sbq[nb];
+                    }
+                    float* srow = p.S + (uint64_t)qq[nb] * p.s_ld;
+                    if (!p.s_compact) {
+                        *reinterpret_cast<float4*>(srow + rbase) = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+                        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+                        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                        if (rb & 1) {
+                            mx = fmaxf(mx, pmax[nb]);
+                            if (lane < 16) srow[(rt * BM + (rb - 1) * 16) / 32] = mx;
+                        } else {
+                            pmax[nb] = mx;
+                        }
+                    }
+                }
+            }
+            stored = true;
+        } else {
+            // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
+            // each query block, scored with the tile's largest (or, for a negative maximum,
+            // smallest) block scale -- never below any of its values' scores
+            const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+            const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
+            bool any = false;
+            int mrb[2];  // (unused lanes' values are never read)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                int m = acc[0][nb][0];
+#pragma unroll
+                for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m;
+                mrb[nb] = m;
+                any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
+            }
+            if (__ballot(any)) {
+                // level 2: per (query block, 16-row block): its maximum, then its rows
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
+#pragma unroll
+                    for (int rb = 0; rb < 8; ++rb) {
+                        const i32x4v_t& x = acc[rb][nb];
+                        const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
+                        const float scr = sc[rb >> 1];
+                        if (!__ballot(((float)bm * scr) * sbq[nb] >= tau[nb])) continue;
+                        if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
+                            flush_ring(nb);
+                            stored = true;
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float v = ((float)x[r] * scr) * sbq[nb];
+                            const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
+                            if (v >= tau[nb] && row < p.n_rows) {
+                                lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
+                                ++ecnt[nb];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
+    }
+    wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
+    if constexpr (EMIT) {
+        flush_ring(0);
+        flush_ring(1);
+    }
+}
+
+}  // namespace bsrlab
