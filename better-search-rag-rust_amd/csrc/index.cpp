@@ -167,18 +167,26 @@ static int index_finish_load(bsr_index* ix) {
         BSR_HIP(launch_rows_to_bf16n(ix->rows.as<float>(), ix->na.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld,
                                      ix->fop.as<uint16_t>(), ix->stream));
     } else {
-        // (+ one tile of slack: the sample pass reads the scales of a whole 128-row tile)
-        BSR_TRY(ix->ascale.ensure((ix->n_pad / kQuantBlock + 128) * sizeof(float)));
+        BSR_TRY(ix->ascale.ensure(ix->n_pad / kQuantBlock * sizeof(float)));
         BSR_HIP(launch_rows_to_i8(ix->rows.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld, ix->fop.as<int8_t>(),
                                   ix->ascale.as<float>(), ix->flags.as<uint32_t>() + 1, ix->stream));
     }
-    // The sample pass reads every kSampleStride-th row: keep those rows contiguous too (1/32
-    // of the operand bytes) so that it streams whole rows instead of 64-byte pieces 24 KiB apart.
+    // The sample pass reads every kSampleStride-th row: those rows, contiguous (1/32 of the
+    // operand bytes), so that it streams whole rows; int8 indexes quantize them with one scale
+    // per filter tile of sampled rows (its epilogue then takes integer maxima).
     const uint64_t n_s = (ix->n + kSampleStride - 1) / kSampleStride;
-    BSR_TRY(ix->fop_s.ensure((size_t)std::max<uint64_t>(n_s, 1) * ix->op_row_bytes));
-    if (n_s)
-        BSR_HIP(hipMemcpy2DAsync(ix->fop_s.p, ix->op_row_bytes, ix->fop.p, (size_t)ix->op_row_bytes * kSampleStride,
-                                 ix->op_row_bytes, n_s, hipMemcpyDeviceToDevice, ix->stream));
+    const uint64_t n_s_pad = round_up(std::max<uint64_t>(n_s, 1), kSampleScaleRows);
+    BSR_TRY(ix->fop_s.ensure((size_t)n_s_pad * ix->op_row_bytes));
+    if (ix->op == kFilterBF16) {
+        if (n_s)
+            BSR_HIP(hipMemcpy2DAsync(ix->fop_s.p, ix->op_row_bytes, ix->fop.p,
+                                     (size_t)ix->op_row_bytes * kSampleStride, ix->op_row_bytes, n_s,
+                                     hipMemcpyDeviceToDevice, ix->stream));
+    } else {
+        BSR_TRY(ix->ascale_s.ensure((size_t)(n_s_pad / kSampleScaleRows) * sizeof(float)));
+        BSR_HIP(launch_rows_to_i8_sample(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->fop_s.as<int8_t>(),
+                                         ix->ascale_s.as<float>(), ix->stream));
+    }
     uint32_t f[2] = {0, 0};
     BSR_HIP(hipMemcpyAsync(f, ix->flags.p, sizeof f, hipMemcpyDeviceToHost, ix->stream));
     BSR_HIP(hipStreamSynchronize(ix->stream));
@@ -382,7 +390,8 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         BSR_TRY(ix->S.ensure((size_t)qpad * s_ld * sizeof(float)));
         g.A = ix->fop_s.as<uint8_t>();  // the sampled rows, contiguous
         g.a_stride = ix->op_row_bytes;
-        g.a_row_mult = kSampleStride;
+        g.a_scale = ix->ascale_s.as<float>();
+        g.a_scale_rows = kSampleScaleRows;
         g.n_rows = n_s;
         g.n_rt = n_rt_s;
         g.S = ix->S.as<float>();
@@ -400,7 +409,8 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     }
     g.A = ix->fop.as<uint8_t>();
     g.a_stride = ix->op_row_bytes;
-    g.a_row_mult = 1;
+    g.a_scale = ix->ascale.as<float>();
+    g.a_scale_rows = kQuantBlock;
     g.n_rows = (uint32_t)n;
     g.n_rt = (uint32_t)((n + BM - 1) / BM);
     g.S = nullptr;

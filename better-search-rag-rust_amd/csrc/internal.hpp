@@ -76,7 +76,8 @@ struct bsr_index {
     bsr::DevBuf rows;   // f32 [n_pad][ld], zero padded: the reference's values
     bsr::DevBuf na;     // f32 [n_pad]: exact magnitudes (src/metrics.rs:154)
     bsr::DevBuf fop;    // filter operand rows: int8 or bf16 [n_pad][ld]
-    bsr::DevBuf fop_s;  // every kSampleStride-th filter operand row, contiguous (sample pass)
+    bsr::DevBuf fop_s;  // every kSampleStride-th row as the sample pass's operand, contiguous
+    bsr::DevBuf ascale_s; // int8: f32 [n_s_pad / kSampleScaleRows] sample operand scales
     bsr::DevBuf ascale; // int8: f32 [n_pad/32] block scales
     bsr::DevBuf flags;  // u32 [2]: row flags, int8 row error bound (f32 bits)
 

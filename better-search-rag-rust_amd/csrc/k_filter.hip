@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                     const uint32_t ql = wc * 64 + n * 32 + (lane & 31);
                     const uint32_t rbase = rt * BM + wr * 128 + m * 32 + 4 * (lane >> 5);
                     if constexpr (!EMIT) {
-                        // sample scores: tile row r is corpus row r * a_row_mult
+                        // sample scores (int8: a_scale per a_scale_rows tile rows)
                         float v[16];
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                             if constexpr (Op::kInt) {
                                 uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
                                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                                s_r = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                                s_r = p.a_scale[tr / p.a_scale_rows];
                             }
                             v[r] = score(acc[m][n][r], s_r, n);
                         }
@@ -455,15 +455,19 @@ __device__ __forceinline__ void qs_wait() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void qs_wait_n(int n) {
+#define BSR_QS_N(N) \
+    case N: qs_wait<N>(); break;
     switch (n) {
-        case 1: qs_wait<1>(); break;
-        case 2: qs_wait<2>(); break;
-        case 3: qs_wait<3>(); break;
+        BSR_QS_N(1) BSR_QS_N(2) BSR_QS_N(3) BSR_QS_N(4) BSR_QS_N(5) BSR_QS_N(6) BSR_QS_N(7) BSR_QS_N(8)
+        BSR_QS_N(9) BSR_QS_N(10) BSR_QS_N(11) BSR_QS_N(12) BSR_QS_N(13) BSR_QS_N(14) BSR_QS_N(15)
         default: qs_wait<0>(); break;
     }
+#undef BSR_QS_N
 }
 
 typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
+
+constexpr int kSampleTilesPerWG = 8;  // sample pass (compact): tiles of maxima staged in LDS
 
 __device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
 
@@ -474,7 +478,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
     constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES];
+    // SAMPLE, compact: the workgroup's maxima [tile][4][256 queries], written to S at the end
+    constexpr int SB_BYTES = EMIT ? 0 : kSampleTilesPerWG * 4 * BN * 4;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES + SB_BYTES];
+    float* const sbuf = reinterpret_cast<float*>(lds + S * SLOT + EM_BYTES);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
@@ -562,6 +569,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         const uint32_t rt = g0 + t * RG;
         float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+        // SAMPLE: one scale for the tile's 128 sampled rows (a scalar load: counted in lgkmcnt,
+        // it leaves the DMA stream's vmcnt waits alone)
+        float sc_tile = 1.0f;
+        if constexpr (!EMIT) sc_tile = p.a_scale[rt * BM / kSampleScaleRows];
 #pragma unroll
         for (int kt = 0; kt < NK; ++kt) {
             const uint32_t jj = t * NK + kt;
@@ -595,38 +606,51 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
         bool stored = false;
         if constexpr (!EMIT) {
-            // sample pass: tile row r is corpus row 32r (a_row_mult == kQuantBlock), whose scale
-            // is a_scale[r]; tail rows (re-reads of the last sampled row) take its scale too
-            const float sc_last = p.a_scale[p.n_rows - 1];
-            float pmax[2] = {0.0f, 0.0f};  // compact: the even row block's maxima
+            // sample pass, one scale per tile: compact = the integer maximum over each 32-row
+            // group (row blocks 2g, 2g+1: the lane's 8 values, then across the four lanes of its
+            // query by two VALU lane swaps), scored once; full = every row's score
+            if (p.s_compact) {
 #pragma unroll
-            for (int rb = 0; rb < 8; ++rb) {
-                const uint32_t rbase = rt * BM + rb * 16 + 4 * (lane >> 4);
-                const float4 s4 = *reinterpret_cast<const float4*>(p.a_scale + rbase);
-                const float srow4[4] = {rbase < p.n_rows ? s4.x : sc_last, rbase + 1 < p.n_rows ? s4.y : sc_last,
-                                        rbase + 2 < p.n_rows ? s4.z : sc_last, rbase + 3 < p.n_rows ? s4.w : sc_last};
+                for (int g = 0; g < 4; ++g)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    float v[4];
+                    for (int nb = 0; nb < 2; ++nb) {
+                        const i32x4v_t& x = acc[2 * g][nb];
+                        const i32x4v_t& y = acc[2 * g + 1][nb];
+                        int m = max(max(max(x[0], x[1]), max(x[2], x[3])), max(max(y[0], y[1]), max(y[2], y[3])));
+                        const auto p16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+                        m = max((int)p16[0], (int)p16[1]);
+                        const auto p32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+                        m = max((int)p32[0], (int)p32[1]);
+                        const float v = ((float)m * sc_tile) * sbq[nb];
+                        if (lane < 16) sbuf[((t % kSampleTilesPerWG) * 4 + g) * BN + (qq[nb] - qt * BN)] = v;
+                    }
+                if (t % kSampleTilesPerWG == kSampleTilesPerWG - 1 || t + 1 == my_rt) {
+                    // every kSampleTilesPerWG tiles: the staged maxima to S, 4 consecutive columns
+                    // per (query, tile) (global stores inside the DMA stream only this often)
+                    __syncthreads();
+                    const uint32_t t0 = t - t % kSampleTilesPerWG, nt = t + 1 - t0;
+                    for (uint32_t i = tid; i < nt * BN; i += NT) {
+                        const uint32_t tt = i / BN, ql = i % BN;
+                        const float4 v = make_float4(sbuf[(tt * 4 + 0) * BN + ql], sbuf[(tt * 4 + 1) * BN + ql],
+                                                     sbuf[(tt * 4 + 2) * BN + ql], sbuf[(tt * 4 + 3) * BN + ql]);
+                        *reinterpret_cast<float4*>(p.S + (uint64_t)(qt * BN + ql) * p.s_ld + (g0 + (t0 + tt) * RG) * 4) = v;
+                    }
+                    stored = true;
+                }
+            } else {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = ((float)acc[rb][nb][r] * srow4[r]) * sbq[nb];
-                    float* srow = p.S + (uint64_t)qq[nb] * p.s_ld;
-                    if (!p.s_compact) {
-                        *reinterpret_cast<float4*>(srow + rbase) = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-                        float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-                        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-                        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-                        if (rb & 1) {
-                            mx = fmaxf(mx, pmax[nb]);
-                            if (lane < 16) srow[(rt * BM + (rb - 1) * 16) / 32] = mx;
-                        } else {
-                            pmax[nb] = mx;
-                        }
+                for (int rb = 0; rb < 8; ++rb) {
+                    const uint32_t rbase = rt * BM + rb * 16 + 4 * (lane >> 4);
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb) {
+                        const i32x4v_t& x = acc[rb][nb];
+                        const float v0 = ((float)x[0] * sc_tile) * sbq[nb], v1 = ((float)x[1] * sc_tile) * sbq[nb];
+                        const float v2 = ((float)x[2] * sc_tile) * sbq[nb], v3 = ((float)x[3] * sc_tile) * sbq[nb];
+                        *reinterpret_cast<float4*>(p.S + (uint64_t)qq[nb] * p.s_ld + rbase) = make_float4(v0, v1, v2, v3);
                     }
                 }
+                stored = true;
             }
-            stored = true;
         } else {
             // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
             // each query block, scored with the tile's largest (or, for a negative maximum,
@@ -755,13 +779,13 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
                 }
             }
         } else {
-            // sample: tile row r is corpus row r * a_row_mult, scale block r * mult / 32
+            // sample: int8 scales per a_scale_rows tile rows
             float v[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 uint32_t tr = g * 32 + (i >> 2) * 16 + 4 * h + (i & 3);
                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                const float sc = p.a_scale[tr / p.a_scale_rows];
                 v[i] = ((float)(i < 4 ? acc0[i] : acc1[i - 4]) * sc) * sbq;
             }
             float* srow = p.S + (uint64_t)q * p.s_ld;
@@ -843,7 +867,7 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
             for (int i = 0; i < 4; ++i) {
                 uint32_t tr = u * 16 + 4 * h + i;
                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                const float sc = p.a_scale[tr / p.a_scale_rows];
                 v[i] = ((float)acc[i] * sc) * sbq;
             }
             float* srow = p.S + (uint64_t)q * p.s_ld;

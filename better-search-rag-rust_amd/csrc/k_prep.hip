@@ -218,6 +218,59 @@ __global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ ro
     if (lane == 0) atomicMax(ea_max, __float_as_uint(f32_round_up(ew * (1.0 + 1e-9) + 1e-12)));
 }
 
+// The sample operand: kSampleScaleRows sampled rows (corpus rows kSampleStride apart) per
+// workgroup, one scale for all of them; rows past the corpus are zero.
+__global__ __launch_bounds__(256) void k_rows_to_i8_sample(const float* __restrict__ rows, uint64_t n,
+                                                           uint32_t dim, uint32_t ld, int8_t* __restrict__ out,
+                                                           float* __restrict__ scales) {
+    __shared__ double s_inv[kSampleScaleRows];
+    __shared__ double s_wmax[4];
+    const uint64_t blk = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    constexpr int kRowsPerWave = kSampleScaleRows / 4;
+    double wmax = 0.0;
+    for (int i = 0; i < kRowsPerWave; ++i) {
+        const int rl = w * kRowsPerWave + i;
+        const uint64_t r = (blk * kSampleScaleRows + rl) * kSampleStride;  // corpus row
+        double ss = 0.0, mx = 0.0;
+        if (r < n) {
+            const float* a = rows + r * ld;
+            for (uint32_t c = lane; c < dim; c += kWave) {
+                const double x = a[c];
+                ss += x * x;
+                mx = fmax(mx, fabs(x));
+            }
+        }
+        ss = wave_sum_f64(ss);
+        mx = wave_max_f64(mx);
+        const double inv = (ss > 0.0 && ss < 1e300) ? 1.0 / sqrt(ss) : 0.0;
+        if (lane == 0) s_inv[rl] = inv;
+        wmax = fmax(wmax, mx * inv);
+    }
+    if (lane == 0) s_wmax[w] = wmax;
+    __syncthreads();
+    const double bmax = fmax(fmax(s_wmax[0], s_wmax[1]), fmax(s_wmax[2], s_wmax[3]));
+    const float sc = bmax > 0.0 ? f32_round_up(bmax / 127.0) : 1.0f;
+    if (t == 0) scales[blk] = sc;
+    const double s = sc;
+    for (int i = 0; i < kRowsPerWave; ++i) {
+        const int rl = w * kRowsPerWave + i;
+        const uint64_t rs = blk * kSampleScaleRows + rl;  // sample row
+        const uint64_t r = rs * kSampleStride;
+        const double inv = s_inv[rl];
+        const float* a = rows + r * ld;
+        for (uint32_t c0 = lane * 4; c0 < ld; c0 += 4 * kWave) {
+            int8_t qv[4] = {0, 0, 0, 0};
+            if (r < n && inv > 0.0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (c0 + j < dim) qv[j] = quant_i8((double)a[c0 + j] * inv, s);
+            }
+            *reinterpret_cast<char4*>(out + rs * ld + c0) = make_char4(qv[0], qv[1], qv[2], qv[3]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Queries: one wave per (padded) query, the whole preparation in one kernel.
 //   1. the caller's row -> LDS (coalesced) and the padded f32 copy qf32[q] (zeros past dim)
@@ -387,6 +440,15 @@ hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint
     const uint64_t blocks = n_pad / kQuantBlock;
     hipLaunchKernelGGL(k_rows_to_i8, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, dim, ld, out, scales,
                        ea_max);
+    return hipGetLastError();
+}
+hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim, uint32_t ld, int8_t* out,
+                                    float* scales, hipStream_t s) {
+    const uint64_t n_s = (n + kSampleStride - 1) / kSampleStride;
+    const uint64_t blocks = (n_s + kSampleScaleRows - 1) / kSampleScaleRows;
+    if (blocks)
+        hipLaunchKernelGGL(k_rows_to_i8_sample, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, dim, ld, out,
+                           scales);
     return hipGetLastError();
 }
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {

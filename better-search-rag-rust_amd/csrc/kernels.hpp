@@ -13,7 +13,7 @@ constexpr uint32_t kRowPad = 256;      // rows are padded to a multiple of this 
 constexpr uint32_t kScanQF = 8;        // queries per exact-scan launch (max)
 constexpr uint32_t kSampleStride = 32; // candidate-threshold sample: every 32nd row
 constexpr uint32_t kQuantBlock = 32;   // rows sharing one int8 scale (one 32-row MFMA block)
-static_assert(kSampleStride == kQuantBlock, "sample pass: sampled row r has scale a_scale[r]");
+constexpr uint32_t kSampleScaleRows = 128; // int8 sample rows sharing one scale (one filter tile)
 constexpr uint32_t kFilterTile = 256;  // MFMA filter tile: 256 corpus rows x 256 queries
 
 // Operand type of the MFMA candidate filter.
@@ -54,6 +54,12 @@ hipError_t launch_rows_to_bf16n(const float* rows, const float* na, uint64_t n, 
 hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint32_t dim,
                              uint32_t ld, int8_t* out, float* scales, uint32_t* ea_max,
                              hipStream_t s);
+// The sample pass's operand: rows 0, kSampleStride, 2 kSampleStride, ... of the corpus,
+// contiguous, int8 with one scale per kSampleScaleRows of them (the sample pass only sets the
+// emission threshold; no certification depends on its quantization).  out: [n_s_pad][ld],
+// scales: [n_s_pad / kSampleScaleRows], n_s_pad = round_up(n_s, kSampleScaleRows).
+hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim, uint32_t ld,
+                                    int8_t* out, float* scales, hipStream_t s);
 // Query preparation: exact |b| (src/metrics.rs:155), flags, padded f32 copy, the filter
 // operand (bf16 or int8 + scale) and the per-query certification bound ebound[q].
 struct QueryPrepArgs {
@@ -78,7 +84,7 @@ struct GemmArgs {
     const uint8_t* A;       // filter rows [n_pad][row_bytes]
     uint64_t a_stride;      // bytes between consecutive tile rows (row_bytes, or x sample stride)
     uint32_t n_rows;        // valid tile rows (n for emit, n_sample for the sample pass)
-    uint32_t a_row_mult;    // corpus row of tile row r = r * a_row_mult (1 emit, 32 sample)
+    uint32_t a_scale_rows;  // int8: tile rows per a_scale entry (kQuantBlock emit, kSampleScaleRows sample)
     const uint8_t* B;       // filter queries [qpad][row_bytes]
     uint32_t row_bytes;     // bytes of one operand row (multiple of 64)
     uint32_t n_rt, n_qt;    // row tiles, query tiles

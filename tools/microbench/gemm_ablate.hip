@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill_f32, dim3(16), dim3(256), 0, 0, bs, (size_t)qpad, 1.0f / (127.0f * 16.0f));
     CHECK(hipDeviceSynchronize());
     GemmArgs g{};
-    g.n_rows = n; g.a_row_mult = 1; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
+    g.n_rows = n; g.a_scale_rows = 32; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
     g.S = reinterpret_cast<float*>(stamp);
     g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;

@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                             if constexpr (Op::kInt) {
                                 uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
                                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                                s_r = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                                s_r = p.a_scale[tr / p.a_scale_rows];
                             }
                             v[r] = score(acc[m][n][r], s_r, n);
                         }
@@ -771,7 +771,7 @@ __device__ __forceinline__ void filter_qs_body(const GemmArgs& p) {
                     for (int r = 0; r < 16; ++r) {
                         uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
                         tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                        v[r] = score(acc[m][n][r], p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]);
+                        v[r] = score(acc[m][n][r], p.a_scale[tr / p.a_scale_rows]);
                     }
                     float* srow = p.S + (uint64_t)(qt * BN + ql) * p.s_ld;
                     if (!p.s_compact) {
@@ -932,7 +932,7 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
             for (int i = 0; i < 8; ++i) {
                 uint32_t tr = g * 32 + (i >> 2) * 16 + 4 * h + (i & 3);
                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                const float sc = p.a_scale[tr / p.a_scale_rows];
                 v[i] = ((float)(i < 4 ? acc0[i] : acc1[i - 4]) * sc) * sbq;
             }
             float* srow = p.S + (uint64_t)q * p.s_ld;
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
             for (int i = 0; i < 4; ++i) {
                 uint32_t tr = u * 16 + 4 * h + i;
                 tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                const float sc = p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock];
+                const float sc = p.a_scale[tr / p.a_scale_rows];
                 v[i] = ((float)acc[i] * sc) * sbq;
             }
             float* srow = p.S + (uint64_t)q * p.s_ld;

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                     for (int r = 0; r < 4; ++r) {
                         uint32_t tr = rbase + r;
                         tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                        v[r] = ((float)acc[rb][nb][r] * p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]) * sbq[nb];
+                        v[r] = ((float)acc[rb][nb][r] * p.a_scale[tr / p.a_scale_rows]) * sbq[nb];
                     }
                     float* srow = p.S + (uint64_t)qq[nb] * p.s_ld;
                     if (!p.s_compact) {

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(512, 1) void k_lab_ring(GemmArgs p) {
                 for (int r = 0; r < 16; ++r) {
                     uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
                     tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                    v[r] = ((float)acc[m][r] * p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]) * sbq;
+                    v[r] = ((float)acc[m][r] * p.a_scale[tr / p.a_scale_rows]) * sbq;
                 }
                 float* srow = p.S + (uint64_t)q * p.s_ld;
                 if (!p.s_compact) {
@@ -464,7 +464,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_ring(GemmArgs p) {
                 for (int r = 0; r < 16; ++r) {
                     uint32_t tr = rbase + (r & 3) + 8 * (r >> 2);
                     tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                    v[r] = ((float)acc[m][r] * p.a_scale[(uint64_t)tr * p.a_row_mult / kQuantBlock]) * sbq;
+                    v[r] = ((float)acc[m][r] * p.a_scale[tr / p.a_scale_rows]) * sbq;
                 }
                 float* srow = p.S + (uint64_t)q * p.s_ld;
                 if (!p.s_compact) {

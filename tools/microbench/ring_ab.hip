@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     bsr::GemmArgs g{};
     g.A = A8; g.B = B8; g.row_bytes = ld; g.a_stride = ld;
-    g.n_rows = n; g.a_row_mult = 1; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
+    g.n_rows = n; g.a_scale_rows = 32; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
     g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
     printf("emitted sets %s\n", sets[0] == sets[1] ? "IDENTICAL" : "DIFFER");
     {
         bsr::GemmArgs gs = g;
-        gs.a_stride = (uint64_t)ld * 32; gs.a_row_mult = 32; gs.n_rows = n_s; gs.n_rt = (n_s + 255) / 256;
+        gs.a_stride = (uint64_t)ld * 32; gs.a_scale_rows = 128; gs.n_rows = n_s; gs.n_rt = (n_s + 255) / 256;
         gs.S = S; gs.s_ld = s_ld; gs.s_compact = 0;
         std::vector<std::vector<float>> sv(2);
         void (*ks[2])(bsr::GemmArgs) = {bsrlab::k_filter_qs8<false, 12, false, 72>, bsr::k_filter_qs16<false, 12>};
@@ -129,6 +129,24 @@ int main(int argc, char** argv) {
     }
     // ---- timing: settle ~2 s, then interleaved rounds
     for (int i = 0; i < 200; ++i) run(vs[i & 1].k, g, tau_emit);
+    if (argc > 5 && strcmp(argv[5], "sample") == 0) {  // the sample pass vs the emit pass on n/32 rows
+        bsr::GemmArgs gs = g;
+        gs.n_rows = n_s; gs.n_rt = (n_s + 255) / 256;
+        const uint32_t n_vals = (n_s + 31) / 32;
+        gs.S = S; gs.s_ld = (n_s + 255) / 256 * 8; gs.s_compact = 1;
+        struct W { const char* name; void (*k)(bsr::GemmArgs); bsr::GemmArgs a; float tau; std::vector<float> t; };
+        std::vector<W> ws = {{"sample compact", bsr::k_filter_qs16<false, 12>, gs, 0.0f, {}},
+                             {"sample full", bsr::k_filter_qs16<false, 12>, gs, 0.0f, {}},
+                             {"emit tau=inf", bsr::k_filter_qs16<true, 12>, gs, 1e9f, {}}};
+        ws[1].a.s_compact = 0; ws[1].a.s_ld = (n_s + 255) / 256 * 256;
+        for (int r = 0; r < rounds; ++r)
+            for (auto& w : ws) w.t.push_back(run(w.k, w.a, w.tau));
+        for (auto& w : ws) {
+            std::sort(w.t.begin(), w.t.end());
+            printf("%-16s rows %u (vals %u)  median %7.4f ms  min %7.4f ms\n", w.name, n_s, n_vals, w.t[w.t.size() / 2], w.t[0]);
+        }
+        return 0;
+    }
     if (argc > 5 && strcmp(argv[5], "sweep") == 0) {  // cost of emission: time vs tau (first two variants)
         for (float tv : {1e9f, 0.145f, 0.14f, 0.135f, 0.13f, 0.125f, 0.12f}) {
             for (int i = 0; i < 2; ++i) {
