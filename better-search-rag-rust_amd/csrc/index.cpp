@@ -125,6 +125,29 @@ static inline void ev_kernel(bsr_index* ix, Events& e, hipEvent_t& a, hipEvent_t
     a = b = nullptr;
     if (profiling(ix) && ix->prof_level >= 1 && e.a) { a = e.a; b = e.b; e.armed = true; }
 }
+// A filter / scan kernel launch timed at profile level >= 1: inside a graph capture the events
+// are recorded on the stream around the launch (event-record nodes: the kernel plus its
+// dispatch gap), otherwise bound to the kernel's own dispatch (hipExtLaunchKernel).
+template <class F>
+static inline hipError_t launch_timed(bsr_index* ix, Events& e, F&& launch) {
+    if (ix->capturing) {
+        const bool timed = profiling(ix) && ix->prof_level >= 1 && e.a;
+        if (timed) {
+            hipError_t r = hipEventRecord(e.a, ix->stream);
+            if (r != hipSuccess) return r;
+        }
+        hipError_t r = launch((hipEvent_t) nullptr, (hipEvent_t) nullptr);
+        if (r != hipSuccess) return r;
+        if (timed) {
+            e.armed = true;
+            return hipEventRecord(e.b, ix->stream);
+        }
+        return hipSuccess;
+    }
+    hipEvent_t e0, e1;
+    ev_kernel(ix, e, e0, e1);
+    return launch(e0, e1);
+}
 static inline void ev_collect(Events& e, double& ms, uint64_t& n, uint64_t launches) {
     if (!e.armed) return;
     float t = 0.0f;
@@ -397,10 +420,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         g.S = ix->S.as<float>();
         g.s_ld = s_ld;
         g.s_compact = compact ? 1u : 0u;
-        hipEvent_t e0, e1;
-        ev_kernel(ix, ix->ev_sample, e0, e1);
-        if (skinny) BSR_HIP(launch_filter_skinny_sample(g, ix->stream, e0, e1));
-        else BSR_HIP(launch_filter_sample(ix->op, g, ix->stream, e0, e1));
+        BSR_HIP(launch_timed(ix, ix->ev_sample, [&](hipEvent_t e0, hipEvent_t e1) {
+            return skinny ? launch_filter_skinny_sample(g, ix->stream, e0, e1)
+                          : launch_filter_sample(ix->op, g, ix->stream, e0, e1);
+        }));
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
                                   ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
     } else {
@@ -418,10 +441,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cand = ix->cand.as<uint64_t>();
     g.cnt = ix->cnt.as<uint32_t>();
     g.cap = cap;
-    hipEvent_t e0, e1;
-    ev_kernel(ix, ix->ev_emit, e0, e1);
-    if (skinny) BSR_HIP(launch_filter_skinny_emit(g, ix->stream, e0, e1));
-    else BSR_HIP(launch_filter_emit(ix->op, g, ix->stream, e0, e1));
+    BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
+        return skinny ? launch_filter_skinny_emit(g, ix->stream, e0, e1)
+                      : launch_filter_emit(ix->op, g, ix->stream, e0, e1);
+    }));
     ev_begin(ix, ix->ev_select);
     BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(), kp,
                                ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), ix->tau_excl.as<float>(),
@@ -551,11 +574,20 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         return BSR_OK;
     };
 
-    const bool graphable = use_filter && n > 0 && nq <= kSkinnyMaxQ && (!profiling(ix) || prof_level == 0);
+    // Every filtered batch is graph-capturable (profile level <= 1: the filter kernels' events
+    // become event-record nodes); level 2 times every stage directly.
+    const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level <= 1);
     SearchGraph& gs = graphs[cur];
-    const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n;
-    if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen) {
+    const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
+                            warm.timed == (profiling(ix) ? prof_level : 0);
+    const int timed_level = profiling(ix) ? prof_level : 0;
+    if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen &&
+        gs.timed == timed_level) {
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
+        if (timed_level >= 1) {  // the captured event-record nodes ran
+            ev_emit.armed = true;
+            ev_sample.armed = gs.sampled;
+        }
         stats.n_candidates = kp_for(k);
         ++graph_replays;
         stats.graph_replay = 1;
@@ -564,7 +596,9 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         if (gs.exec) { (void)hipGraphExecDestroy(gs.exec); gs.exec = nullptr; }
         BSR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         const uint64_t gen0 = g_alloc_gen;
+        capturing = true;
         const int rc = enqueue_search();
+        capturing = false;
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(stream, &graph);
         if (rc != BSR_OK) { if (graph) (void)hipGraphDestroy(graph); return rc; }
@@ -576,13 +610,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(BSR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen};
+        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level, ev_sample.armed};
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         ++graph_replays;
         stats.graph_replay = 1;
     } else {
         BSR_TRY(enqueue_search());
-        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen};
+        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, false};
     }
     next_status_clean = true;
     BSR_HIP(hipStreamSynchronize(stream));

@@ -106,16 +106,18 @@ struct bsr_index {
     bsr::Events ev_emit, ev_sample, ev_select, ev_rescore, ev_scan, ev_total;
     int prof_level = 2;  // bsr_index_set_profile
 
-    // Small filtered batches (<= kSkinnyMaxQ queries, the latency path) replay a captured
-    // hipGraph of query prep -> filter -> select -> rescore -> finalize -> D2H instead of
-    // ~9 launches.  One graph per result buffer; captured on the second search of a shape
+    // Filtered batches replay a captured hipGraph of query prep -> filter -> select -> rescore
+    // -> finalize -> D2H instead of ~9 launches.  One graph per result buffer; captured on the second search of a shape
     // (the first sizes every buffer), dropped when the shape or any allocation changes.
     struct SearchGraph {
         hipGraphExec_t exec = nullptr;
         uint32_t nq = 0, k = 0;
         const float* qsrc = nullptr;
         uint64_t n = 0, gen = 0;
+        int timed = 0;         // profile level it was captured at (event-record nodes at >= 1)
+        bool sampled = false;  // it contains the sample pass (its events armed on replay)
     };
+    bool capturing = false;    // a search is being captured into a graph
     SearchGraph graphs[2];
     SearchGraph warm;  // the last direct search of a graphable shape (no exec)
     uint64_t graph_replays = 0;

@@ -670,28 +670,35 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
             }
             if (__ballot(any)) {
-                // level 2: per (query block, 16-row block): its maximum, then its rows
+                // level 2: per (query block, 16-row block) its maximum against tau -- eight
+                // independent scores, then one uniform branch per passing row block -- and that
+                // block's 4 rows appended without branches (every key is written to the next
+                // ring slot, the count advances only for passing rows)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
                     if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
+                    bool pass_rb[8];
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
                         const i32x4v_t& x = acc[rb][nb];
                         const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
-                        const float scr = sc[rb >> 1];
-                        if (!__ballot(((float)bm * scr) * sbq[nb] >= tau[nb])) continue;
+                        pass_rb[rb] = ((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb];
+                    }
+#pragma unroll
+                    for (int rb = 0; rb < 8; ++rb) {
+                        if (!__ballot(pass_rb[rb])) continue;
                         if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
                             flush_ring(nb);
                             stored = true;
                         }
+                        const i32x4v_t& x = acc[rb][nb];
+                        const float scr = sc[rb >> 1];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const float v = ((float)x[r] * scr) * sbq[nb];
                             const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
-                            if (v >= tau[nb] && row < p.n_rows) {
-                                lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
-                                ++ecnt[nb];
-                            }
+                            lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
+                            ecnt[nb] += (v >= tau[nb] && row < p.n_rows) ? 1u : 0u;
                         }
                     }
                 }

@@ -15,7 +15,7 @@ typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
 
 __device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
 
-// VAR bits (tooling): 1 no DMA, 2 no epilogue
+// VAR bits (tooling): 1 no DMA, 2 no epilogue, 4 epilogue level 1 only, 8 no candidate stores
 template <bool EMIT, int NK, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 mrb[nb] = m;
                 any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
             }
-            if (__ballot(any)) {
+            if (!(VAR & 4) && __ballot(any)) {
                 // level 2: per (query block, 16-row block): its maximum, then its rows
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                             const float v = ((float)x[r] * scr) * sbq[nb];
                             const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
                             if (v >= tau[nb] && row < p.n_rows) {
-                                lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
+                                if (!(VAR & 8)) lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
                                 ++ecnt[nb];
                             }
                         }

@@ -70,10 +70,11 @@ int main(int argc, char** argv) {
     std::vector<V> vs = {
         {"qs8 (round 1)", bsrlab::k_filter_qs8<true, 12, false, 72>, {}},
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, {}},
-        {"qs8 noDMA noEpi", bsrlab::k_filter_qs8<true, 12, false, 78>, {}},
-        {"qs16 noDMA noEpi", bsrlab::k_filter_qs16<true, 12, 3>, {}},
-        {"qs16 noEpi", bsrlab::k_filter_qs16<true, 12, 2>, {}},
-        {"ring", bsrlab::k_filter_ring<true, 12>, {}},
+        {"lab qs16", bsrlab::k_filter_qs16<true, 12, 0>, {}},
+        {"lab qs16 noEpi", bsrlab::k_filter_qs16<true, 12, 2>, {}},
+        {"lab qs16 level1", bsrlab::k_filter_qs16<true, 12, 4>, {}},
+        {"lab qs16 noStore", bsrlab::k_filter_qs16<true, 12, 8>, {}},
+        {"lab qs16 noDMA noEpi", bsrlab::k_filter_qs16<true, 12, 3>, {}},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
