@@ -283,8 +283,9 @@ def main():
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
-                if pm.get("rows") == n_local and pm.get("queries") == Q and pm.get("filter") == args.filter:
-                    traffic = pm.get("hbm_bytes_per_launch")
+                for e in pm.get("entries", [pm]):
+                    if e.get("rows") == n_local and e.get("queries") == Q and e.get("filter") == args.filter:
+                        traffic = e.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         if args.filter == "i8" and Q <= 16:

@@ -1,34 +1,84 @@
-// k_qs16_lab.hip -- TOOLING (candidate for the product): the query-stationary int8 filter of
-// round 1 (k_filter_qs8: 8 waves, 32 queries per wave in registers, 128-row tiles through an
-// 8-slot LDS ring, one s_barrier per two slices, steady LDS-DMA stream) with the
-// v_mfma_i32_16x16x64_i8 shape instead of v_mfma_i32_32x32x32_i8 (MI355X_MICROARCH.md,
-// DVFS item 7: the 16x16 shape holds a higher clock at about equal cycles per op).
-// Per slice a wave reads 8 A fragments (16 rows x 64 bytes each, one ds_read_b128) and issues
-// 16 MFMAs (8 row blocks x 2 query blocks of 16).  LDS chunk swizzle for the 16-row read
-// pattern: rows 8..15 of every 16-row group XOR their chunk with 2 (conflict-free for the
-// four ds_read_b128 lane groups).
+// k_qs16_lab.hip -- TOOLING (candidate for the product): the product's query-stationary
+// int8 emit filter (k_filter.hip, bsr::k_filter_qs16<true, NK>) with a STAGED emission
+// epilogue instead of the two-level per-row one.
+//
+// Product epilogue: level 1 = the lane's integer maximum over its 32 values per query
+// block against tau, one ballot per tile; level 2 (when any lane passes) = per 16-row block
+// maxima, then per passing block its 4 rows into a private per-lane LDS ring.  Level 2 runs
+// on most wave-tiles at the product's emission rate (~1 emitted row per 32 queries x 128
+// rows) and all 8 waves wait for the slowest at the next barrier.
+// Staged: a lane that passes level 1 writes its 32 raw int32 values (8 x ds_write_b128) and
+// one meta record (first row, query, tau, query scale) into a per-wave staging area (slot =
+// count + mbcnt of the pass mask); the wave then scores two staged entries per iteration,
+// one value per lane, and compacts passing (key, query) pairs into a per-wave key ring
+// (ballot + mbcnt).  The key ring goes to the global per-query lists at the end (or when
+// full) with one global atomic per (wave, query).  Emitted SETS equal the product's.
+// VAR bits: 1 = no level-2 work at all (level 1 only, results discarded: cost floor);
+// 2 = level-1 maxima folded into the last slice's MFMA stream (row block rb - 2 after group rb);
+// 4 = staged entries scored later, one step (2 entries) per slice inside the next tile's
+// MFMA stream (the two waves of a SIMD at different groups) instead of in the epilogue;
+// 8 = one barrier per FOUR slices (12-slot ring, 8 slices ahead; NK % 4 == 0);
+// 16 = timing probe: the final key-ring flush (global atomics + stores) skipped.
 // Included after the product k_filter.hip (uses its types and helpers).
 namespace bsrlab {
 using namespace bsr;
 
-typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
+// compiler-only ordering of this wave's LDS accesses across lanes (the LDS executes a wave's
+// operations in order, so no wait is needed)
+__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
+// LDS accesses of the emission path as inline asm: the compiler cannot prove them disjoint
+// from the in-flight LDS-DMA slots and would drain the whole DMA stream (vmcnt(0)) first
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ void ds_st128(uint32_t a, i32x4v_t v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ds_st64(uint32_t a, uint64_t v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ds_st32(uint32_t a, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ int ds_ld32_wait(uint32_t a) {
+    int r;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+__device__ __forceinline__ i32x4v_t ds_ld128_wait(uint32_t a) {
+    i32x4v_t r;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
 
-__device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
-
-// VAR bits (tooling): 1 no DMA, 2 no epilogue, 4 epilogue level 1 only, 8 no candidate stores
-template <bool EMIT, int NK, int VAR = 0>
-__global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
-    constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
-    constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
-    constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
-    constexpr bool kNoDMA = VAR & 1, kNoEpi = VAR & 2;
+template <int NK, int VAR = 0, int NW = 8>
+__global__ __launch_bounds__(512, 1) void k_filter_qs16s(GemmArgs p) {
+    // BAR slices per barrier: 2 (product: 8 slots, 6 ahead) or 4 (VAR & 8: 12 slots, 8 ahead).
+    // Slot reuse needs A <= S - BAR; at a barrier (slice jj, after group 5) slices <= jj + BAR + 1
+    // must have landed, leaving A - 1 - (BAR + 1) younger DMAs in flight.
+    constexpr int BAR = (VAR & 8) ? 4 : 2;
+    constexpr int S = (VAR & 8) ? 12 : 8, A = (VAR & 8) ? 8 : 6;
+    constexpr int WAITN = A - 2 - BAR;
+    static_assert(A <= S - BAR && NK % BAR == 0, "ring geometry");
+    // NW waves of 32 queries per workgroup: 8 (one workgroup per CU) or 4 (two per CU, each
+    // with its own ring and barriers: one computes while the other is in its epilogue)
+    static_assert(NW == 8 || NW == 4, "4 or 8 waves");
+    constexpr int BM = 128, BN = 32 * NW, NT = 64 * NW, SLOT = BM * kSliceB;
+    constexpr int ND = 8 / NW;           // 1-KiB DMA instructions per wave per slice
+    constexpr int STG = NW == 8 ? 16 : 8;   // staged (lane, query block) entries per wave
+    constexpr int KR = NW == 8 ? 256 : 128; // key-ring entries per wave
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
-    constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES];
+    // ONE LDS object (separate __shared__ variables get alias scopes, and the compiler then
+    // waits for the LDS-DMA stream before every fragment read): ring | staging | key ring
+    constexpr int STG_V = S * SLOT, STG_M = STG_V + NW * STG * 32 * 4, KR_KEY = STG_M + NW * STG * 16;
+    constexpr int KR_Q = KR_KEY + NW * KR * 8, KR_CNT = KR_Q + NW * KR * 4, LDS_BYTES = KR_CNT + NW * 32 * 4;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
+    // staging: [wave][entry][32 int32 values], meta [wave][entry] = {row0, q, tau, sbq}
+    auto stg_v = reinterpret_cast<int32_t (*)[STG][32]>(lds + STG_V);
+    auto stg_m = reinterpret_cast<uint32_t (*)[STG][4]>(lds + STG_M);
+    auto kr_key = reinterpret_cast<uint64_t (*)[KR]>(lds + KR_KEY);
+    auto kr_q = reinterpret_cast<uint32_t (*)[KR]>(lds + KR_Q);      // local query | position << 8
+    auto kr_cnt = reinterpret_cast<uint32_t (*)[32]>(lds + KR_CNT);  // per-query counts, then bases
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
-    uint32_t ecnt[2] = {0, 0};
 
     const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const uint32_t G = (gridDim.x >> 3) / p.n_qt;
@@ -39,83 +89,138 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     const uint32_t RG = 8 * G;
     const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
     const uint32_t J = my_rt * NK;
+    const uint32_t qw0 = qt * BN + w * 32;  // the wave's first query
 
-    // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
-    // qt*256 + 32w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
     uint32_t qq[2];
     i32x4v_t fb[2][NK];
     float tau[2], sbq[2];
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
-        qq[nb] = qt * BN + w * 32 + nb * 16 + (lane & 15);
+        qq[nb] = qw0 + nb * 16 + (lane & 15);
         const uint8_t* src = p.B + (uint64_t)qq[nb] * p.row_bytes + 16 * (lane >> 4);
 #pragma unroll
         for (int kt = 0; kt < NK; ++kt) fb[nb][kt] = *reinterpret_cast<const i32x4v_t*>(src + 64 * kt);
-        tau[nb] = EMIT ? p.tau[qq[nb]] : 0.0f;
+        tau[nb] = p.tau[qq[nb]];
         sbq[nb] = p.b_scale[qq[nb]];
     }
-    auto flush_ring = [&](int nb) {
-        const uint32_t nn = ecnt[nb];
-        if (nn) {
-            const uint32_t gp = atomicAdd(p.cnt + qq[nb], nn);
-            for (uint32_t i = 0; i < nn; ++i)
-                if (gp + i < p.cap) p.cand[(uint64_t)qq[nb] * p.cap + gp + i] = lkeys[(nb * CAP + i) * NT];
+    uint32_t scnt = 0, kcnt = 0;  // wave-uniform
+    // key ring -> global lists: per-query counts in LDS, one global atomic per query, scatter
+    auto flush_keys = [&]() {
+        if (lane < 32) kr_cnt[w][lane] = 0;
+        wave_lds_order();
+        for (uint32_t i = lane; i < kcnt; i += 64) {
+            const uint32_t ql = kr_q[w][i] & 31u;
+            const uint32_t pos = atomicAdd(&kr_cnt[w][ql], 1u);
+            kr_q[w][i] = ql | (pos << 8);
         }
-        ecnt[nb] = 0;
+        wave_lds_order();
+        if (lane < 32) {
+            const uint32_t c = kr_cnt[w][lane];
+            kr_cnt[w][lane] = c ? atomicAdd(p.cnt + qw0 + lane, c) : 0u;
+        }
+        wave_lds_order();
+        for (uint32_t i = lane; i < kcnt; i += 64) {
+            const uint32_t ql = kr_q[w][i] & 31u, gp = kr_cnt[w][ql] + (kr_q[w][i] >> 8);
+            if (gp < p.cap) p.cand[(uint64_t)(qw0 + ql) * p.cap + gp] = kr_key[w][i];
+        }
+        kcnt = 0;
     };
 
-    // LDS-DMA: wave w fills rows 16w .. 16w+15 of each slice (1 KiB per instruction); the
-    // source chunk is XOR-swizzled so that LDS chunk position p holds global chunk p ^ swz.
-    const uint32_t lrow = w * 16 + (lane >> 2);
-    const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
-    uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
+    // wave w fills rows 16 * ND * w .. + 16 * ND - 1 of every slice (ND instructions)
+    auto dma_off = [&](int i) {
+        const uint32_t lrow = (w * ND + i) * 16 + (lane >> 2);
+        return lrow * (uint32_t)p.a_stride + ((lane & 3) ^ qs16_swz(lrow)) * 16;
+    };
+    const uint32_t aoff_dma0 = dma_off(0), aoff_dma1 = ND > 1 ? dma_off(1) : 0u;
     uint32_t iss_ti = 0, iss_kt = 0;
     __amdgpu_buffer_rsrc_t rsrc_a;
     auto set_issue_tile = [&]() {
         const uint32_t rt = g0 + iss_ti * RG;
         rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
                                                    BM * (uint32_t)p.a_stride, 0x00020000);
-        if (!EMIT) {
-            const uint32_t r = rt * BM + lrow < p.n_rows ? lrow : p.n_rows - 1 - rt * BM;
-            aoff_dma = r * (uint32_t)p.a_stride + lchunk;
-        }
     };
     auto issue_dma = [&](uint32_t jj) {
-        uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma, iss_kt * kSliceB, 0, 0);
+        uint8_t* la = lds + (jj % S) * SLOT + wu * ND * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma0, iss_kt * kSliceB, 0, 0);
+        if (ND > 1)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)(la + 1024), 16, aoff_dma1, iss_kt * kSliceB, 0, 0);
         if (++iss_kt == NK) {
             iss_kt = 0;
             ++iss_ti;
             if (iss_ti < my_rt) set_issue_tile();
         }
     };
-    // A fragment of row block rb (rows 16rb .. +15): lane -> row 16rb + (lane & 15), chunk
-    // lane >> 4; the swizzle depends on row & 15 only, so block rb is at a constant 1 KiB step
     const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
-    // four fragment registers, read four row blocks ahead: block rb of slice jj lands in
-    // fa[rb & 3] while the MFMAs of block rb - 4 (the same slice, or the previous one) run
     i32x4v_t fa[4];
     auto read_frag = [&](uint32_t jj, int rb) {
-        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (kNoDMA ? 0 : jj % S) * SLOT + rb * 1024 + aoff0);
+        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
     };
 
     i32x4v_t acc[8][2];
     if (my_rt) set_issue_tile();
     const uint32_t pre = J ? (uint32_t)A : 0u;
     for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
-    qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
+    qs_barrier(pre >= (uint32_t)(BAR + 1) ? (pre - (BAR + 1)) * ND : 0);  // slices 0 .. BAR landed everywhere
     if (J)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
 
+    // staged entries [dr, scnt) wait to be scored with the block scales psc of their tile
+    uint32_t dr = 0;
+    float psc[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+    // score staged entries e0, e0 + 1 (lane -> entry e0 + lane/32, value lane%32)
+    auto drain_step = [&](uint32_t e0) {
+        const uint32_t vi = lane & 31, rb = vi >> 2;
+        const float scr = rb < 4 ? (rb < 2 ? psc[0] : psc[1]) : (rb < 6 ? psc[2] : psc[3]);
+        const uint32_t e = e0 + (lane >> 5);
+        const bool valid = e < scnt;
+        const uint32_t ec = valid ? e : e0;
+        const int v = ds_ld32_wait(lds_addr(&stg_v[w][ec][vi]));
+        const i32x4v_t m4 = ds_ld128_wait(lds_addr(&stg_m[w][ec][0]));
+        const uint32_t row = (uint32_t)m4[0] + (rb << 4) + (vi & 3);
+        const float sv = ((float)v * scr) * __int_as_float(m4[3]);
+        const bool ok = valid && sv >= __int_as_float(m4[2]) && row < p.n_rows;
+        const uint64_t bm = __ballot(ok);
+        if (ok) {
+            const uint32_t ks = kcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+            ds_st64(lds_addr(&kr_key[w][ks]), score_key(sv, row));
+            ds_st32(lds_addr(&kr_q[w][ks]), (uint32_t)m4[1]);
+        }
+        kcnt += (uint32_t)__builtin_popcountll(bm);
+    };
+    // every staged entry scored (flushing the key ring when it could overflow)
+    auto drain_all = [&]() -> bool {
+        bool st = false;
+        wave_lds_order();
+        for (; dr < scnt; dr += 2) {
+            if (kcnt > (uint32_t)(KR - 64)) {
+                flush_keys();
+                st = true;
+            }
+            drain_step(dr);
+        }
+        scnt = dr = 0;
+        return st;
+    };
+    // the wave pair on one SIMD (w, w + 4) drains at different groups of a slice
+    const int drain_rb = (wu >> 2) ? 2 : 6;
+
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
-        float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-        if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+        const float4 scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+        int mx[2] = {INT32_MIN, INT32_MIN};  // level-1 maxima, folded into the last slice
+        auto fold = [&](int rb) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const i32x4v_t& x = acc[rb][nb];
+                mx[nb] = max(mx[nb], max(max(x[0], x[1]), max(x[2], x[3])));
+            }
+        };
 #pragma unroll
         for (int kt = 0; kt < NK; ++kt) {
             const uint32_t jj = t * NK + kt;
-            const bool bar_slice = (kt & 1) == 1;
+            const bool bar_slice = (kt % BAR) == BAR - 1;
 #pragma unroll
             for (int rb = 0; rb < 8; ++rb) {
 #pragma unroll
@@ -129,110 +234,78 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (rb < 4) read_frag(jj, rb + 4);
-                else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
-                // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
-                // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
-                if (!kNoDMA && (bar_slice ? rb == 6 : rb == 1)) issue_dma(jj + A);
-                // barrier (odd slices, after group 5): slices <= jj + 3 landed everywhere (the
-                // reads before the next barrier reach rows 0-1 of slice jj + 3); in flight: the
-                // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
-                // the tile's scale load
-                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
+                else read_frag(jj + 1, rb - 4);
+                if (bar_slice ? rb == 6 : rb == 1) issue_dma(jj + A);
+                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(WAITN * ND + (kt <= A - 2 - BAR ? 1 : 0));
+                if ((VAR & 2) && kt == NK - 1 && rb >= 2) fold(rb - 2);
+                if ((VAR & 4) && kt >= 1 && kt <= NK - 2 && rb == drain_rb) {
+                    // deferred scoring of the previous tile's staged entries, in the MFMA stream
+                    if (dr < scnt && kcnt <= (uint32_t)(KR - 64)) {
+                        wave_lds_order();
+                        drain_step(dr);
+                        dr += 2;
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if constexpr (kNoEpi) {
+        // ---- epilogue, level 1: the lane's maximum over its 32 values per query block
+        const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
+        const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+        const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
+        if (VAR & 2) {
+            fold(6);
+            fold(7);
+        } else {
 #pragma unroll
-            for (int rb = 0; rb < 8; ++rb) asm volatile("" ::"v"(acc[rb][0]), "v"(acc[rb][1]));
+            for (int rb = 0; rb < 8; ++rb) fold(rb);
+        }
+        bool pass[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) pass[nb] = ((float)mx[nb] * (mx[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
+        if constexpr (VAR & 1) {
+            asm volatile("" ::"v"(pass[0]), "v"(pass[1]));
             continue;
         }
-        // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
-        const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
         bool stored = false;
-        if constexpr (!EMIT) {
-            float pmax[2] = {0.0f, 0.0f};  // compact: the even row block's maxima
+        if (dr < scnt) stored |= drain_all();  // the previous tile's entries, not yet scored
+        scnt = dr = 0;
 #pragma unroll
-            for (int rb = 0; rb < 8; ++rb) {
-                const uint32_t rbase = rt * BM + rb * 16 + 4 * (lane >> 4);
+        for (int i = 0; i < 4; ++i) psc[i] = sc[i];
+        // stage the passing lanes' 32 values (slot = count + rank in the pass mask)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    float v[4];
+        for (int nb = 0; nb < 2; ++nb) {
+            uint64_t m = __ballot(pass[nb]);
+            while (m) {
+                const uint32_t room = STG - scnt;
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                const bool mine = ((m >> lane) & 1ull) && rank < room;
+                if (mine) {
+                    const uint32_t e = scnt + rank;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        uint32_t tr = rbase + r;
-                        tr = tr < p.n_rows ? tr : p.n_rows - 1;
-                        v[r] = ((float)acc[rb][nb][r] * p.a_scale[tr / p.a_scale_rows]) * sbq[nb];
-                    }
-                    float* srow = p.S + (uint64_t)qq[nb] * p.s_ld;
-                    if (!p.s_compact) {
-                        *reinterpret_cast<float4*>(srow + rbase) = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-                        float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-                        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-                        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-                        if (rb & 1) {
-                            mx = fmaxf(mx, pmax[nb]);
-                            if (lane < 16) srow[(rt * BM + (rb - 1) * 16) / 32] = mx;
-                        } else {
-                            pmax[nb] = mx;
-                        }
-                    }
+                    for (int rb = 0; rb < 8; ++rb) ds_st128(lds_addr(&stg_v[w][e][rb * 4]), acc[rb][nb]);
+                    const i32x4v_t mt = {(int)(rt * BM + 4 * (lane >> 4)), nb * 16 + (lane & 15),
+                                         __float_as_int(tau[nb]), __float_as_int(sbq[nb])};
+                    ds_st128(lds_addr(&stg_m[w][e][0]), mt);
                 }
-            }
-            stored = true;
-        } else {
-            // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
-            // each query block, scored with the tile's largest (or, for a negative maximum,
-            // smallest) block scale -- never below any of its values' scores
-            const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
-            const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
-            bool any = false;
-            int mrb[2];  // (unused lanes' values are never read)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                int m = acc[0][nb][0];
-#pragma unroll
-                for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m;
-                mrb[nb] = m;
-                any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
-            }
-            if (!(VAR & 4) && __ballot(any)) {
-                // level 2: per (query block, 16-row block): its maximum, then its rows
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
-#pragma unroll
-                    for (int rb = 0; rb < 8; ++rb) {
-                        const i32x4v_t& x = acc[rb][nb];
-                        const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
-                        const float scr = sc[rb >> 1];
-                        if (!__ballot(((float)bm * scr) * sbq[nb] >= tau[nb])) continue;
-                        if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
-                            flush_ring(nb);
-                            stored = true;
-                        }
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float v = ((float)x[r] * scr) * sbq[nb];
-                            const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
-                            if (v >= tau[nb] && row < p.n_rows) {
-                                if (!(VAR & 8)) lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
-                                ++ecnt[nb];
-                            }
-                        }
-                    }
-                }
+                const uint64_t took = __ballot(mine);
+                m &= ~took;
+                scnt += (uint32_t)__builtin_popcountll(took);
+                if (scnt == STG) stored |= drain_all();
             }
         }
+        if (!(VAR & 4) && scnt) stored |= drain_all();
         if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
     }
-    wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
-    if constexpr (EMIT) {
-        flush_ring(0);
-        flush_ring(1);
+    if (scnt) (void)drain_all();
+    wait_vm0();
+    wave_lds_order();
+    if (VAR & 16) {  // timing probe: no global candidate writes at the end (results incomplete)
+        if (kcnt == 12345) p.cnt[0] = kcnt;
+        return;
     }
+    flush_keys();
 }
 
 }  // namespace bsrlab

@@ -1,5 +1,6 @@
 // Microbenchmark + cross-check (tooling): the product filter kernel (k_filter.hip, namespace
-// bsr: k_filter_qs16) against the round-1 kernel (k_filter_lab.hip) and the lab variants on a
+// bsr: k_filter_qs16) against the lab variants (k_qs16_lab.hip) and the round-1 kernel
+// (k_filter_lab.hip) on a
 // synthetic int8 shard, interleaved in one process (same clocks), after a clock settle.
 // Checks that both kernels emit the same candidate set per query (sorted keys equal) and the
 // same sample scores, then times them.
@@ -13,6 +14,7 @@
 
 #include <stdio.h>
 #include <string.h>
+
 
 #include <algorithm>
 #include <vector>
@@ -66,25 +68,32 @@ int main(int argc, char** argv) {
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
 
-    struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; };
+    struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; int nw; };
     std::vector<V> vs = {
-        {"qs8 (round 1)", bsrlab::k_filter_qs8<true, 12, false, 72>, {}},
-        {"qs16 (product)", bsr::k_filter_qs16<true, 12>, {}},
-        {"lab qs16", bsrlab::k_filter_qs16<true, 12, 0>, {}},
-        {"lab qs16 noEpi", bsrlab::k_filter_qs16<true, 12, 2>, {}},
-        {"lab qs16 level1", bsrlab::k_filter_qs16<true, 12, 4>, {}},
-        {"lab qs16 noStore", bsrlab::k_filter_qs16<true, 12, 8>, {}},
-        {"lab qs16 noDMA noEpi", bsrlab::k_filter_qs16<true, 12, 3>, {}},
+        {"qs16 (product)", bsr::k_filter_qs16<true, 12>, {}, 8},
+        {"qs16 staged (lab)", bsrlab::k_filter_qs16s<12, 0>, {}, 8},
+        {"staged+fold", bsrlab::k_filter_qs16s<12, 2>, {}, 8},
+        {"staged, no end flush", bsrlab::k_filter_qs16s<12, 16>, {}, 8},
+        {"staged+fold no flush", bsrlab::k_filter_qs16s<12, 18>, {}, 8},
+        {"level-1 only", bsrlab::k_filter_qs16s<12, 1>, {}, 8},
+        {"qs8 (round 1)", bsrlab::k_filter_qs8<true, 12, false, 72>, {}, 8},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    auto run = [&](void (*k)(bsr::GemmArgs), const bsr::GemmArgs& a, float tv) -> float {
+    auto run = [&](void (*k)(bsr::GemmArgs), const bsr::GemmArgs& a0, float tv, int nw = 8) -> float {
+        // nw = 4: 128-query workgroups, two per CU
+        bsr::GemmArgs a = a0;
+        uint32_t gr = grid;
+        if (nw == 4) {
+            a.n_qt = qpad / 128;
+            gr = 8 * ((64 / a.n_qt) * a.n_qt);
+        }
         std::vector<float> ht(qpad, tv);
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
         CHECK(hipMemset(cnt, 0, qpad * 4));
         CHECK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, a);
+        hipLaunchKernelGGL(k, dim3(gr), dim3(64 * nw), 0, 0, a);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
@@ -92,9 +101,10 @@ int main(int argc, char** argv) {
         return ms;
     };
     // ---- cross-check: emitted candidate sets and sample scores
-    std::vector<std::vector<uint64_t>> sets(2);
-    for (int i = 0; i < 2; ++i) {
-        run(vs[i].k, g, tau_emit);
+    const int n_check = 3;  // product + the staged variants (emitting)
+    std::vector<std::vector<uint64_t>> sets(n_check);
+    for (int i = 0; i < n_check; ++i) {
+        run(vs[i].k, g, tau_emit, vs[i].nw);
         std::vector<uint32_t> hc(qpad);
         CHECK(hipMemcpy(hc.data(), cnt, qpad * 4, hipMemcpyDeviceToHost));
         std::vector<uint64_t> hk((size_t)qpad * cap);
@@ -110,7 +120,8 @@ int main(int argc, char** argv) {
         }
         printf("[%s] emitted per query %.1f\n", vs[i].name, tot / nq);
     }
-    printf("emitted sets %s\n", sets[0] == sets[1] ? "IDENTICAL" : "DIFFER");
+    for (int i = 1; i < n_check; ++i)
+        printf("emitted sets %s vs %s: %s\n", vs[i].name, vs[0].name, sets[0] == sets[i] ? "IDENTICAL" : "DIFFER");
     {
         bsr::GemmArgs gs = g;
         gs.a_stride = (uint64_t)ld * 32; gs.a_scale_rows = 128; gs.n_rows = n_s; gs.n_rt = (n_s + 255) / 256;
@@ -129,7 +140,7 @@ int main(int argc, char** argv) {
         printf("sample scores %s (%zu differ)\n", bad ? "DIFFER" : "IDENTICAL", bad);
     }
     // ---- timing: settle ~2 s, then interleaved rounds
-    for (int i = 0; i < 200; ++i) run(vs[i & 1].k, g, tau_emit);
+    for (int i = 0; i < 200; ++i) run(vs[i & 1].k, g, tau_emit, vs[i & 1].nw);
     if (argc > 5 && strcmp(argv[5], "sample") == 0) {  // the sample pass vs the emit pass on n/32 rows
         bsr::GemmArgs gs = g;
         gs.n_rows = n_s; gs.n_rt = (n_s + 255) / 256;
@@ -152,7 +163,7 @@ int main(int argc, char** argv) {
         for (float tv : {1e9f, 0.145f, 0.14f, 0.135f, 0.13f, 0.125f, 0.12f}) {
             for (int i = 0; i < 2; ++i) {
                 std::vector<float> t;
-                for (int r = 0; r < rounds; ++r) t.push_back(run(vs[i].k, g, tv));
+                for (int r = 0; r < rounds; ++r) t.push_back(run(vs[i].k, g, tv, vs[i].nw));
                 std::sort(t.begin(), t.end());
                 std::vector<uint32_t> hc(qpad);
                 CHECK(hipMemcpy(hc.data(), cnt, qpad * 4, hipMemcpyDeviceToHost));
@@ -166,7 +177,7 @@ int main(int argc, char** argv) {
     for (float tv : {1e9f, tau_emit}) {
         for (auto& v : vs) v.t.clear();
         for (int r = 0; r < rounds; ++r)
-            for (auto& v : vs) v.t.push_back(run(v.k, g, tv));
+            for (auto& v : vs) v.t.push_back(run(v.k, g, tv, v.nw));
         for (auto& v : vs) {
             std::sort(v.t.begin(), v.t.end());
             const float med = v.t[v.t.size() / 2];

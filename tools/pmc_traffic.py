@@ -5,7 +5,11 @@ on gfx950 FETCH_SIZE (KB) reports half of the bytes of a wide coalesced read
 (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for 16-B stores.  FETCH_SIZE and
 WRITE_SIZE are collected in separate passes (TCC counter slots).
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <rows> <queries> <filter> <out.json>
+
+out.json keeps one entry per (rows, queries, filter) shard shape under "entries", so the
+bench finds the traffic of each rank's shard at every N; a rerun replaces its entry.
 """
+import os
 import csv
 import glob
 import json
@@ -39,7 +43,17 @@ def main():
     if emit:
         res["dominant_kernel"] = emit[0]
         res["hbm_bytes_per_launch"] = res["kernels"][emit[0]]["hbm_bytes_corrected"]
-    json.dump(res, open(out, "w"), indent=1)
+    entries = []
+    if os.path.exists(out):
+        try:
+            old = json.load(open(out))
+            entries = old.get("entries", [old] if "rows" in old else [])
+        except (OSError, ValueError):
+            entries = []
+    key = (res["rows"], res["queries"], res["filter"])
+    entries = [e for e in entries if (e.get("rows"), e.get("queries"), e.get("filter")) != key] + [res]
+    entries.sort(key=lambda e: (e.get("filter"), e.get("queries"), -e.get("rows", 0)))
+    json.dump({"entries": entries}, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}))
 
 
