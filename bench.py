@@ -332,7 +332,7 @@ def main():
                 "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank)" +
                                ("" if world == 1 else f" + {args.comm.upper()} all-gather of the partial lists"
                                                       " + root merge"),
-                "filter": ("int8 MFMA (v_mfma_i32_32x32x32_i8) candidates" if args.filter == "i8" else
+                "filter": ("int8 MFMA (v_mfma_i32_16x16x64_i8) candidates" if args.filter == "i8" else
                            "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates") +
                           f", exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)",
             },
