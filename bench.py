@@ -212,12 +212,14 @@ def main():
     # only (bound to their dispatch: the roofline's launch durations).
     index.set_profile(1)
     index.profile(reset=True)
-    stats_fb = 0
+    stats_fb = stats_rescued = 0
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        stats_fb += index.last_stats().n_fallback
+        ls = index.last_stats()
+        stats_fb += ls.n_fallback
+        stats_rescued += ls.n_rescued
     barrier()
     elapsed = time.perf_counter() - t0
     prof = index.profile(reset=True)
@@ -354,6 +356,7 @@ def main():
                 "exact_scan": round(prof_scan.scan_ms / max(prof_scan.scan_launches, 1), 4),
                 "local_search_total": round(prof_scan.search_ms / max(prof_scan.searches, 1), 4)},
             "fallback_queries_per_step_rank0": stats_fb / args.steps,
+            "rescued_queries_per_step_rank0": stats_rescued / args.steps,
             "candidates_per_query": st.n_candidates,
             "self_query_rank1": bool(res_i[0, 0] == 0 and res_d[0, 0] == 0.0),
             "emitted_per_query_rank0": round(st.n_emitted / max(Q, 1), 1),

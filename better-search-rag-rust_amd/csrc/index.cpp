@@ -469,6 +469,24 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     ra.fail_cnt = status + kStFail;
     ra.fail_list = ix->fail.as<uint32_t>();
     BSR_HIP(launch_rescore(ra, ix->stream));
+    // Second chance, in the same stream (and graph): a query that failed certification is
+    // rescored over EVERY row it emitted (~4k'), certified against tau0 -- far less than a
+    // scan.  The failed count is read on the device, so no host round trip; what fails here
+    // too goes to fail2 (exact scan, host-driven).
+    RescoreArgs rb = ra;
+    rb.n_items = nq;
+    rb.n_items_dev = status + kStFail;
+    rb.qlist = ix->fail.as<uint32_t>();
+    rb.cand_rows = nullptr;
+    rb.ncand = nullptr;
+    rb.tau_excl = nullptr;
+    rb.cand_keys = ix->cand.as<uint64_t>();
+    rb.cnt = ix->cnt.as<uint32_t>();
+    rb.cap = cap;
+    rb.tau0 = ix->tau.as<float>();
+    rb.fail_cnt = status + kStFail2;
+    rb.fail_list = ix->fail2.as<uint32_t>();
+    BSR_HIP(launch_rescore(rb, ix->stream));
     ev_end(ix, ix->ev_rescore);
     return BSR_OK;
 }
@@ -568,7 +586,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
             BSR_TRY(run_filter(ix, nq, qpad, k));
         }
         BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
-                                stream));
+                                (use_filter && n > 0) ? cnt.as<uint32_t>() : nullptr, d_status, stream));
         ev_end(ix, ev_total);
         BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
         return BSR_OK;
@@ -623,7 +641,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     // Later rounds (second-chance rescore, scan) finalize and read back again, directly.
     auto finalize_and_read = [&]() -> int {
         BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
-                                stream));
+                                nullptr, d_status, stream));
         next_status_clean = true;
         BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
         BSR_HIP(hipStreamSynchronize(stream));
@@ -640,38 +658,11 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
     }
     if (use_filter) {
         stats.n_emitted = st[kStEmitted];
-        uint32_t nfail = st[kStFail];
-        const uint32_t* fail_dev = fail.as<uint32_t>();
-        if (nfail) {
-            // Second chance: an uncertified query rescored over EVERY row it emitted
-            // (certified against the emission threshold tau0) -- ~4k' rows instead of a scan.
-            RescoreArgs ra{};
-            ra.rows = rows.as<float>();
-            ra.ld = ld;
-            ra.dim = dim;
-            ra.na = na.as<float>();
-            ra.qf32 = qf32.as<float>();
-            ra.nb = nb.as<float>();
-            ra.n_items = nfail;
-            ra.qlist = fail.as<uint32_t>();
-            ra.cand_keys = cand.as<uint64_t>();
-            ra.cnt = cnt.as<uint32_t>();
-            ra.cap = cap_for(k);
-            ra.tau0 = tau.as<float>();
-            ra.k = k;
-            ra.ebound = ebound.as<float>();
-            ra.out_keys = keys.as<uint64_t>();
-            ra.fail_cnt = d_status + kStFail2;
-            ra.fail_list = fail2.as<uint32_t>();
-            ev_begin(ix, ev_rescore);
-            BSR_HIP(launch_rescore(ra, stream));
-            ev_end(ix, ev_rescore);
-            stats.n_rescued = nfail;
-            BSR_TRY(finalize_and_read());
-            nfail = st[kStFail2];
-            stats.n_rescued -= nfail;
-            fail_dev = fail2.as<uint32_t>();
-        }
+        // st[kStFail] queries failed the first certification and were rescored over every
+        // emitted row in the same launch sequence; st[kStFail2] of them failed again.
+        const uint32_t nfail = st[kStFail2];
+        const uint32_t* fail_dev = fail2.as<uint32_t>();
+        stats.n_rescued = st[kStFail] - nfail;
         if (nfail) {
             // Uncertified queries, and queries the filter cannot serve (zero/tiny/huge |b|),
             // take the exact full scan: the reference's arithmetic on every row.

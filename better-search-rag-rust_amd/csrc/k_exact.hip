@@ -9,6 +9,9 @@
 
 #include <math.h>
 
+#include <algorithm>
+#include <type_traits>
+
 namespace bsr {
 
 static inline uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap = 65536) {
@@ -66,81 +69,152 @@ __device__ __forceinline__ void seq_chunk(const float* __restrict__ my, const fl
     }
 }
 
-template <int E>
-__global__ __launch_bounds__(64) void k_rescore(RescoreArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[64 * 68 + 64];  // 64 rows + the query chunk
-    float* ldq = lds + 64 * 68;
-    if (blockIdx.x >= a.n_items) return;
-    const uint32_t q = a.qlist ? a.qlist[blockIdx.x] : blockIdx.x;
-    const int lane = threadIdx.x;
-    // mode B (every emitted candidate) or mode A (the k' selected ones)
-    const bool all = a.cand_keys != nullptr;
-    const uint32_t cnt = all ? a.cnt[q] : a.ncand[q];
-    const bool overflow = all && cnt > a.cap;  // rows were dropped: nothing can be certified
-    const uint32_t c = overflow ? 0u : cnt;
-    const float* bq = a.qf32 + (uint64_t)q * a.ld;
-    const float mag_b = a.nb[q];
-    const uint32_t ld = a.ld, dim = a.dim, nch = ld / 64;
-    const float* rows = a.rows;
+// This wave's LDS stage for the candidate rows is private to it (W > 1 waves per workgroup
+// each walk their own 64 candidates): ordering inside the wave is enough.
+// The LDS executes one wave's operations in order, so only the compiler must not move LDS
+// accesses across this point.  (A fence or __syncthreads would also wait for every global
+// load in flight -- vmcnt(0) -- and serialise the two-chunk prefetch below.)
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
-    WaveTopK<E> L;
-    L.init();
-    uint64_t thr = kKeyNone;
-    for (uint32_t base = 0; base < c; base += kWave) {
-        const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
-        const uint32_t myrow = all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc]) : a.cand_rows[(uint64_t)q * a.kp + cc];
-        float acc[1] = {-0.0f}, mx[1] = {0.0f};
-        uint32_t lrow[16];
+// W waves per workgroup, one query per workgroup at a time: wave w takes candidates
+// w*64 + lane, + 64W, ...; the W per-wave lists merge through LDS.  W = 1: one wave per
+// query (the k' selected candidates, every query).  W = 8: the queries that failed
+// certification, every emitted row (~4k'), their count read on the device
+// (a.n_items_dev), so the launch needs no host round trip.  P chunks of candidate rows are
+// loaded ahead (rows of 768 floats; other widths: 2).
+template <int E, int W, int P>
+__global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
+    constexpr int STAGE = 64 * 68;  // 64 rows (stride 68) per wave
+    constexpr int QMAX = 1024;      // the whole query in LDS (rows up to 1024 floats)
+    __shared__ __attribute__((aligned(16))) float lds_all[W * STAGE + QMAX];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float* const lds = lds_all + w * STAGE;
+    float* const ldq_all = lds_all + W * STAGE;
+    const uint32_t n_items = a.n_items_dev ? *a.n_items_dev : a.n_items;
+    for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+        const uint32_t q = a.qlist ? a.qlist[item] : item;
+        // the query, once per item (its loads are not behind the candidate prefetch); rows
+        // longer than QMAX read it from global memory instead
+        const bool qlds = a.ld <= (uint32_t)QMAX;
+        if (qlds)
+            for (uint32_t c = threadIdx.x; c < a.ld; c += 64 * W) ldq_all[c] = a.qf32[(uint64_t)q * a.ld + c];
+        if constexpr (W > 1) __syncthreads();
+        else wave_sync();
+        // mode B (every emitted candidate) or mode A (the k' selected ones)
+        const bool all = a.cand_keys != nullptr;
+        const uint32_t cnt = all ? a.cnt[q] : a.ncand[q];
+        const bool overflow = all && cnt > a.cap;  // rows were dropped: nothing can be certified
+        const uint32_t c = overflow ? 0u : cnt;
+        const float mag_b = a.nb[q];
+        const uint32_t ld = a.ld, dim = a.dim, nch = ld / 64;
+        const float* rows = a.rows;
+
+        WaveTopK<E> L;
+        L.init();
+        uint64_t thr = kKeyNone;
+        // QL: the query chunk from the LDS copy (typed as LDS after inlining: ds_read), else
+        // from global memory (rows longer than QMAX)
+        // NC > 0: the chunk count as a constant (ld = 64 NC; the loop below fully unrolls, so
+        // the prefetch's vmcnt waits are exact); NC = 0: any ld
+        auto scan = [&](auto ql_tag, auto nc_tag) {
+            constexpr bool QL = decltype(ql_tag)::value;
+            constexpr uint32_t NC = decltype(nc_tag)::value;
+            const uint32_t nchk = NC ? NC : nch;
+            for (uint32_t base = 64 * w; base < c; base += 64 * W) {
+                const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
+                const uint32_t myrow = all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc])
+                                           : a.cand_rows[(uint64_t)q * a.kp + cc];
+                float acc[1] = {-0.0f}, mx[1] = {0.0f};
+                uint32_t lrow[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
-        // two chunks of loads in flight (register sets A / B), one LDS stage
-        f32x4_t preA[16], preB[16];
-        load_cand_chunk(preA, rows, ld, lrow, 0, lane);
-        if (nch > 1) load_cand_chunk(preB, rows, ld, lrow, 1, lane);
-        auto step = [&](f32x4_t (&pre)[16], uint32_t ch) {
-            __syncthreads();
+                for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
+                // one chunk: this wave's 64 rows x 64 elements through its LDS stage, then each
+                // lane walks its row in index order
+                auto step = [&](f32x4_t (&pre)[16], uint32_t ch, uint32_t ahead) {
+                    wave_sync();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int L16 = i * 64 + lane;
-                *reinterpret_cast<f32x4_t*>(lds + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
+                    for (int i = 0; i < 16; ++i) {
+                        const int L16 = i * 64 + lane;
+                        *reinterpret_cast<f32x4_t*>(lds + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
+                    }
+                    wave_sync();
+                    if (ch + ahead < nchk) load_cand_chunk(pre, rows, ld, lrow, ch + ahead, lane);
+                    const float* const bb[1] = {QL ? ldq_all + ch * 64 : a.qf32 + (uint64_t)q * ld + ch * 64};
+                    const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
+                    seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
+                };
+                if constexpr (NC > 0) {
+                    // P chunks of loads in flight (a register ring; the loop unrolls fully, so
+                    // the vmcnt waits are counted)
+                    constexpr uint32_t PP = (uint32_t)P < NC ? (uint32_t)P : NC;
+                    f32x4_t pre[PP][16];
+#pragma unroll
+                    for (uint32_t ch = 0; ch < PP; ++ch) load_cand_chunk(pre[ch], rows, ld, lrow, ch, lane);
+#pragma unroll
+                    for (uint32_t ch = 0; ch < NC; ++ch) step(pre[ch % PP], ch, PP);
+                } else {
+                    // any ld: two chunks in flight (register sets A / B)
+                    f32x4_t preA[16], preB[16];
+                    load_cand_chunk(preA, rows, ld, lrow, 0, lane);
+                    if (nchk > 1) load_cand_chunk(preB, rows, ld, lrow, 1, lane);
+                    for (uint32_t ch = 0; ch < nchk; ch += 2) {
+                        step(preA, ch, 2);
+                        if (ch + 1 < nchk) step(preB, ch + 1, 2);
+                    }
+                }
+                const float d = finish_distance(acc[0], mx[0], a.na[myrow], mag_b);
+                L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
             }
-            ldq[lane] = bq[ch * 64 + lane];  // the query chunk (LDS broadcast reads)
-            __syncthreads();
-            if (ch + 2 < nch) load_cand_chunk(pre, rows, ld, lrow, ch + 2, lane);
-            const float* const bb[1] = {ldq};
-            const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
-            seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
         };
-        for (uint32_t ch = 0; ch < nch; ch += 2) {
-            step(preA, ch);
-            if (ch + 1 < nch) step(preB, ch + 1);
+        if (qlds && nch == 12) scan(std::true_type{}, std::integral_constant<uint32_t, 12>{});
+        else if (qlds) scan(std::true_type{}, std::integral_constant<uint32_t, 0>{});
+        else scan(std::false_type{}, std::integral_constant<uint32_t, 0>{});
+        if constexpr (W > 1) {
+            // the W lists (k <= 64E keys each) through LDS, merged by wave 0
+            static_assert(W * 64 * E * 8 <= (int)sizeof(lds_all), "merge area");
+            uint64_t* part = reinterpret_cast<uint64_t*>(lds_all);
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; ++e) part[(w * E + e) * 64 + lane] = L.v[e];
+            __syncthreads();
+            if (w == 0) {
+                WaveTopK<E> M;
+                M.init();
+                uint64_t mt = kKeyNone;
+                for (int src = 0; src < W; ++src)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) M.offer(part[(src * E + e) * 64 + lane], (int)a.k, mt);
+                L = M;
+                thr = mt;
+            }
+            __syncthreads();  // part is the next item's LDS stage
         }
-        const float d = finish_distance(acc[0], mx[0], a.na[myrow], mag_b);
-        L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
-    }
-    L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
-
-    if (lane == 0) {
-        // Certification: every row outside the candidate set has approximate
-        // cosine <= tau_x, hence reference cosine <= tau_x + E_q and reference distance
-        // >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must lie strictly below
-        // that, and no excluded row can be element-wise identical to the query.  Mode B:
-        // every emitted row is a candidate, so tau_x is the emission threshold tau0.
-        const float tx = overflow ? INFINITY : (all ? a.tau0[q] : a.tau_excl[q]);
-        const double ebound = (double)a.ebound[q];
-        bool ok;
-        if (tx == -INFINITY) {
-            ok = true;  // every row of the shard was a candidate
-        } else if (!(tx < INFINITY) || thr == kKeyNone) {
-            ok = false;
-        } else {
-            const double dk = (double)key_dist(thr);
-            ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
-                 (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
-        }
-        if (!ok) {
-            const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
-            a.fail_list[pos] = q;
+        if (w == 0) {
+            L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
+            if (lane == 0) {
+                // Certification: every row outside the candidate set has
+                // approximate cosine <= tau_x, hence reference cosine <= tau_x + E_q and
+                // reference distance >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must
+                // lie strictly below that, and no excluded row can be element-wise identical to
+                // the query.  Mode B: every emitted row is a candidate, so tau_x is the
+                // emission threshold tau0.
+                const float tx = overflow ? INFINITY : (all ? a.tau0[q] : a.tau_excl[q]);
+                const double ebound = (double)a.ebound[q];
+                bool ok;
+                if (tx == -INFINITY) {
+                    ok = true;  // every row of the shard was a candidate
+                } else if (!(tx < INFINITY) || thr == kKeyNone) {
+                    ok = false;
+                } else {
+                    const double dk = (double)key_dist(thr);
+                    ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
+                         (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
+                }
+                if (!ok) {
+                    const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
+                    a.fail_list[pos] = q;
+                }
+            }
         }
     }
 }
@@ -310,9 +384,17 @@ __global__ __launch_bounds__(256) void k_merge_parts(const uint64_t* __restrict_
 
 __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* __restrict__ out_idx, float* __restrict__ out_dist,
-                           uint32_t* __restrict__ out_count, uint32_t* __restrict__ status) {
+                           uint32_t* __restrict__ out_count, uint32_t* __restrict__ status,
+                           const uint32_t* __restrict__ emit_cnt, uint32_t* __restrict__ cur_status) {
     const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (e < kStWords) status[e] = 0;  // the status words of the NEXT search's result buffer
+    if (emit_cnt && blockIdx.x == 0 && threadIdx.x < kWave) {
+        // rows emitted by the filter over the batch (a statistic; one wave, no atomics)
+        uint32_t sum = 0;
+        for (uint32_t q = threadIdx.x; q < nq; q += kWave) sum += emit_cnt[q];
+        for (int off = 32; off > 0; off >>= 1) sum += (uint32_t)__shfl_xor((int)sum, off, kWave);
+        if (threadIdx.x == 0) cur_status[kStEmitted] = sum;
+    }
     if (e >= (uint64_t)nq * k) return;
     const uint32_t q = (uint32_t)(e / k), i = (uint32_t)(e - (uint64_t)q * k);
     const uint32_t cnt = (uint64_t)k < n ? k : (uint32_t)n;
@@ -349,13 +431,22 @@ __global__ void k_cosine_pair(const float* __restrict__ a, uint32_t la, const fl
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     if (!a.n_items) return hipSuccess;
     const uint32_t e = (a.k + 63) / 64;
+    // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
+    const bool dev = a.n_items_dev != nullptr;
+    const dim3 g(dev ? std::min<uint32_t>(a.n_items, kRescoreAllGrid) : a.n_items), b(dev ? 512 : 64);
+#define BSR_RESCORE(E)                                                              \
+    do {                                                                            \
+        if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);           \
+        else hipLaunchKernelGGL((k_rescore<E, 1, 2>), g, b, 0, s, a);               \
+    } while (0)
     switch (e) {
-        case 1: hipLaunchKernelGGL(k_rescore<1>, dim3(a.n_items), dim3(64), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_rescore<2>, dim3(a.n_items), dim3(64), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_rescore<3>, dim3(a.n_items), dim3(64), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_rescore<4>, dim3(a.n_items), dim3(64), 0, s, a); break;
+        case 1: BSR_RESCORE(1); break;
+        case 2: BSR_RESCORE(2); break;
+        case 3: BSR_RESCORE(3); break;
+        case 4: BSR_RESCORE(4); break;
         default: return hipErrorInvalidValue;
     }
+#undef BSR_RESCORE
     return hipGetLastError();
 }
 
@@ -413,10 +504,10 @@ hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t
 
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n, uint64_t offset,
                            uint64_t* out_idx, float* out_dist, uint32_t* out_count, uint32_t* status,
-                           hipStream_t s) {
+                           const uint32_t* emit_cnt, uint32_t* cur_status, hipStream_t s) {
     const uint64_t total = (uint64_t)nq * k;
     hipLaunchKernelGGL(k_finalize, dim3(grid_for(total, 256)), dim3(256), 0, s, keys, nq, k, n, offset,
-                       out_idx, out_dist, out_count, status);
+                       out_idx, out_dist, out_count, status, emit_cnt, cur_status);
     return hipGetLastError();
 }
 

@@ -305,11 +305,24 @@ __global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, 
     const float* src = q + (uint64_t)qi * dim;
     float* dst = qf32 + (uint64_t)qi * ld;
     bool bad = false;
-    for (uint32_t c = lane; c < ld; c += kWave) {
-        const float v = (real && c < dim) ? src[c] : 0.0f;
-        bad |= !isfinite(v);
-        dst[c] = v;
-        if (staged) row[c] = v;
+    // 16 loads per lane in flight, then their stores (rows up to 1024 floats: one round)
+    constexpr int B = 16;
+    for (uint32_t c0 = 0; c0 < ld; c0 += B * kWave) {
+        float v[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const uint32_t c = c0 + j * kWave + lane;
+            v[j] = (real && c < dim) ? src[c] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const uint32_t c = c0 + j * kWave + lane;
+            if (c < ld) {
+                bad |= !isfinite(v[j]);
+                dst[c] = v[j];
+                if (staged) row[c] = v[j];
+            }
+        }
     }
     bad = __ballot(bad) != 0;
     __syncthreads();

@@ -128,7 +128,9 @@ struct RescoreArgs {
     const float* na;            // row magnitudes
     const float* qf32;          // queries [qpad][ld]
     const float* nb;            // query magnitudes
-    uint32_t n_items;           // queries to process (the grid)
+    uint32_t n_items;           // queries to process (the grid), or the bound on *n_items_dev
+    const uint32_t* n_items_dev;  // non-null: the item count is read on the device (a status
+                                  // word written by an earlier kernel of the same stream)
     const uint32_t* qlist;      // query id of item b (nullptr: b)
     // mode A, the k' selected candidates: cand_rows[q*kp + i], i < ncand[q]; tau_excl[q]
     const uint32_t* cand_rows;
@@ -147,6 +149,8 @@ struct RescoreArgs {
     uint32_t* fail_cnt;         // uncertified queries: count (a status word) and list
     uint32_t* fail_list;
 };
+// Workgroups of the device-counted rescore (failed certifications, usually a few queries).
+constexpr uint32_t kRescoreAllGrid = 128;
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s);
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold
 // grid * kScanQF * k keys.
@@ -158,9 +162,12 @@ hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t
                               uint32_t nqf, uint32_t k, uint64_t* out_keys, hipStream_t s);
 // Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
 // result buffer the next search will use.
+// status: the NEXT search's status words (zeroed); emit_cnt (optional): per-query emitted
+// counts, summed into cur_status[kStEmitted].
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* out_idx, float* out_dist,
-                           uint32_t* out_count, uint32_t* status, hipStream_t s);
+                           uint32_t* out_count, uint32_t* status, const uint32_t* emit_cnt,
+                           uint32_t* cur_status, hipStream_t s);
 hipError_t launch_cosine_pair(const float* a, uint32_t la, const float* b, uint32_t lb,
                               float* out, hipStream_t s);
 

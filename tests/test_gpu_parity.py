@@ -114,6 +114,7 @@ def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags
     (50000, 96, 17, 200),
     (100000, 768, 24, 10),  # large shard: compact sample (maxima over 32 sampled rows)
     (5000, 40, 16, 10),     # 64-byte int8 rows: one K slice per tile
+    (6000, 1100, 20, 10),   # rows longer than the rescore's LDS query copy (1024 floats)
 ])
 def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
     rng = np.random.default_rng(7 * n + k)

@@ -23,6 +23,15 @@
 namespace bsrlab {
 using namespace bsr;
 
+// A wave-uniform 16-byte load through the scalar data cache (a LOAD: counted in lgkmcnt,
+// so it leaves the LDS-DMA stream's vmcnt accounting alone); the wait is part of it.
+__device__ __forceinline__ float4 smem_load_f32x4(const float* p) {
+    typedef __attribute__((ext_vector_type(4))) float f4_t;
+    f4_t v;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // compiler-only ordering of this wave's LDS accesses across lanes (the LDS executes a wave's
 // operations in order, so no wait is needed)
 __device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
@@ -305,6 +314,292 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16s(GemmArgs p) {
         if (kcnt == 12345) p.cnt[0] = kcnt;
         return;
     }
+    flush_keys();
+}
+
+
+// ------------------------------------------------------------------------------------
+// SKEWED wave groups (candidate for the product).  The two waves on each SIMD (w, w + 4)
+// belong to groups A (waves 0-3) and B (waves 4-7); group B consumes the shared slice
+// stream L = NK/2 slices behind group A (its query fragments loaded in rotated K order, so
+// the register index of slice kt stays static), so the groups' tile epilogues alternate:
+// while one group scores its tile, the other keeps the SIMD's MFMA pipe busy.  The ring
+// holds S = 14 slots (A + L + 1 <= S: after the barrier of slice jj every wave is done with
+// slices <= jj - L).  Emission as k_filter_qs16s (staged per-wave entries, key ring).
+// Accumulators are zeroed explicitly after each epilogue (no C = 0 first MFMA).
+// ------------------------------------------------------------------------------------
+template <int NK>
+__global__ __launch_bounds__(512, 1) void k_filter_qs16k(GemmArgs args) {
+    // the arguments the lambdas below use, as locals (a reference to the by-value kernel
+    // argument would put a copy of it in scratch memory, and scratch loads count in vmcnt)
+    const uint8_t* const pA = args.A;
+    const uint8_t* const pB = args.B;
+    const uint64_t a_stride = args.a_stride, row_bytes = args.row_bytes;
+    const uint32_t n_rows = args.n_rows, n_qt = args.n_qt, cap = args.cap;
+    const float* const a_scale = args.a_scale;
+    const float* const b_scale = args.b_scale;
+    const float* const tau_in = args.tau;
+    uint64_t* const cand = args.cand;
+    uint32_t* const cntp = args.cnt;
+    constexpr int S = 14, A = 6, L = NK / 2;
+    static_assert(NK % 4 == 0 && NK >= 4 && NK <= 12, "NK in {4, 8, 12}: L even");
+    static_assert(A + L + 1 <= S, "slot reuse");
+    constexpr int BM = 128, BN = kFilterTile, SLOT = BM * kSliceB;
+    constexpr int STG = 16, KR = 192;
+    constexpr int STG_V = S * SLOT, STG_M = STG_V + 8 * STG * 32 * 4, KR_KEY = STG_M + 8 * STG * 16;
+    constexpr int KR_Q = KR_KEY + 8 * KR * 8, KR_CNT = KR_Q + 8 * KR * 4, LDS_BYTES = KR_CNT + 8 * 32 * 4;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
+    auto stg_v = reinterpret_cast<int32_t (*)[STG][32]>(lds + STG_V);
+    auto stg_m = reinterpret_cast<uint32_t (*)[STG][4]>(lds + STG_M);
+    auto kr_key = reinterpret_cast<uint64_t (*)[KR]>(lds + KR_KEY);
+    auto kr_q = reinterpret_cast<uint32_t (*)[KR]>(lds + KR_Q);
+    auto kr_cnt = reinterpret_cast<uint32_t (*)[32]>(lds + KR_CNT);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t grp = wu >> 2;            // 0: group A, 1: group B (L slices behind)
+    const uint32_t lag = grp * L;
+
+    const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const uint32_t G = (gridDim.x >> 3) / n_qt;
+    const uint32_t n_rt = (n_rows + BM - 1) / BM;
+    const bool active = slot < G * n_qt;
+    const uint32_t qt = active ? slot % n_qt : 0;
+    const uint32_t g0 = xcd * G + (active ? slot / n_qt : 0);
+    const uint32_t RG = 8 * G;
+    const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
+    const uint32_t JA = my_rt * NK;          // slices of group A's stream
+    const uint32_t X = my_rt ? JA + L : 0;   // loop positions (group B finishes L later)
+    const uint32_t qw0 = qt * BN + w * 32;
+
+    // query fragments; group B's in rotated K order: fb[nb][kt] = K slice (kt + lag) % NK
+    uint32_t qq[2];
+    i32x4v_t fb[2][NK];
+    float tau[2], sbq[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        qq[nb] = qw0 + nb * 16 + (lane & 15);
+        const uint8_t* src = pB + (uint64_t)qq[nb] * row_bytes + 16 * (lane >> 4);
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) {
+            const uint32_t ks = (kt + lag) % NK;
+            fb[nb][kt] = *reinterpret_cast<const i32x4v_t*>(src + 64 * ks);
+        }
+        tau[nb] = tau_in[qq[nb]];
+        sbq[nb] = b_scale[qq[nb]];
+    }
+    // these loads complete here, visibly to the compiler (s_waitcnt vmcnt(0), as a builtin):
+    // otherwise its first use in an epilogue, far into the DMA stream, gets a vmcnt(0)
+    __builtin_amdgcn_s_waitcnt(0xF70);
+    uint32_t scnt = 0, kcnt = 0;
+    auto flush_keys = [&]() __attribute__((always_inline)) {
+        if (lane < 32) kr_cnt[w][lane] = 0;
+        wave_lds_order();
+        for (uint32_t i = lane; i < kcnt; i += 64) {
+            const uint32_t ql = kr_q[w][i] & 31u;
+            const uint32_t pos = atomicAdd(&kr_cnt[w][ql], 1u);
+            kr_q[w][i] = ql | (pos << 8);
+        }
+        wave_lds_order();
+        if (lane < 32) {
+            const uint32_t c = kr_cnt[w][lane];
+            kr_cnt[w][lane] = c ? atomicAdd(cntp + qw0 + lane, c) : 0u;
+        }
+        wave_lds_order();
+        for (uint32_t i = lane; i < kcnt; i += 64) {
+            const uint32_t ql = kr_q[w][i] & 31u, gp = kr_cnt[w][ql] + (kr_q[w][i] >> 8);
+            if (gp < cap) cand[(uint64_t)(qw0 + ql) * cap + gp] = kr_key[w][i];
+        }
+        kcnt = 0;
+    };
+
+    const uint32_t lrow = w * 16 + (lane >> 2);
+    const uint32_t aoff_dma = lrow * (uint32_t)a_stride + ((lane & 3) ^ qs16_swz(lrow)) * 16;
+    uint32_t iss_ti = 0, iss_kt = 0;
+    __amdgpu_buffer_rsrc_t rsrc_a;
+    auto set_issue_tile = [&]() __attribute__((always_inline)) {
+        const uint32_t rt = g0 + iss_ti * RG;
+        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(pA + (uint64_t)rt * BM * a_stride), 0,
+                                                   BM * (uint32_t)a_stride, 0x00020000);
+    };
+    auto issue_dma = [&](uint32_t jj) __attribute__((always_inline)) {
+        uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma, iss_kt * kSliceB, 0, 0);
+        if (++iss_kt == NK) {
+            iss_kt = 0;
+            ++iss_ti;
+            if (iss_ti < my_rt) set_issue_tile();
+        }
+    };
+    const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
+    i32x4v_t fa[4];
+    // this wave's slice at loop position x is x - lag (slot (x + S - lag) % S)
+    auto read_frag = [&](uint32_t x, int rb) __attribute__((always_inline)) {
+        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + ((x + S - lag) % S) * SLOT + rb * 1024 + aoff0);
+    };
+
+    i32x4v_t acc[8][2];
+#define zero_acc()                                                                                \
+    do {                                                                                          \
+        _Pragma("unroll") for (int rb = 0; rb < 8; ++rb)                                          \
+            _Pragma("unroll") for (int nb = 0; nb < 2; ++nb) acc[rb][nb] = i32x4v_t{0, 0, 0, 0};  \
+    } while (0)
+    zero_acc();
+    if (my_rt) set_issue_tile();
+    const uint32_t pre = X ? (uint32_t)A : 0u;
+    for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
+    qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
+    if (X)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
+
+    // the tile's 32-row block scales (uniform; read through the constant address space, i.e.
+    // scalar loads counted in lgkmcnt, outside the DMA stream's vmcnt)
+    float sc0 = 1.0f, sc1 = 1.0f, sc2 = 1.0f, sc3 = 1.0f;
+#define load_scales(U)                                                                            \
+    do {                                                                                          \
+        const uint32_t rt_s = __builtin_amdgcn_readfirstlane(g0 + (U) * RG);                      \
+        const float4 v_s = smem_load_f32x4(a_scale + (uint64_t)rt_s * (BM / kQuantBlock));       \
+        sc0 = v_s.x; sc1 = v_s.y; sc2 = v_s.z; sc3 = v_s.w;                                       \
+    } while (0)
+    // tile U's epilogue: level 1 (lane maxima), staging of passing lanes, scoring; sets
+    // STORED when global stores / atomics were issued (a macro: no closures in the loop)
+#define BSR_QS16K_DRAIN(STORED)                                                                   \
+    do {                                                                                          \
+        wave_lds_order();                                                                         \
+        const uint32_t vi = lane & 31, rbv = vi >> 2;                                             \
+        const float scr = rbv < 4 ? (rbv < 2 ? sc0 : sc1) : (rbv < 6 ? sc2 : sc3);               \
+        for (uint32_t e0 = 0; e0 < scnt; e0 += 2) {                                               \
+            if (kcnt > (uint32_t)(KR - 64)) {                                                     \
+                flush_keys();                                                                     \
+                STORED = true;                                                                    \
+            }                                                                                     \
+            const uint32_t e = e0 + (lane >> 5);                                                  \
+            const bool valid = e < scnt;                                                          \
+            const uint32_t ec = valid ? e : e0;                                                   \
+            const int v = ds_ld32_wait(lds_addr(&stg_v[w][ec][vi]));                              \
+            const i32x4v_t m4 = ds_ld128_wait(lds_addr(&stg_m[w][ec][0]));                        \
+            const uint32_t row = (uint32_t)m4[0] + (rbv << 4) + (vi & 3);                         \
+            const float sv = ((float)v * scr) * __int_as_float(m4[3]);                            \
+            const bool ok = valid && sv >= __int_as_float(m4[2]) && row < n_rows;                 \
+            const uint64_t bm = __ballot(ok);                                                     \
+            if (ok) {                                                                             \
+                const uint32_t ks = kcnt + __builtin_amdgcn_mbcnt_hi(                             \
+                                               (uint32_t)(bm >> 32),                              \
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));      \
+                ds_st64(lds_addr(&kr_key[w][ks]), score_key(sv, row));                            \
+                ds_st32(lds_addr(&kr_q[w][ks]), (uint32_t)m4[1]);                                 \
+            }                                                                                     \
+            kcnt += (uint32_t)__builtin_popcountll(bm);                                           \
+        }                                                                                         \
+        scnt = 0;                                                                                 \
+    } while (0)
+#define BSR_QS16K_EPILOGUE(U, STORED)                                                             \
+    do {                                                                                          \
+        const uint32_t rt_e = g0 + (U) * RG;                                                      \
+        const float sc_hi = fmaxf(fmaxf(sc0, sc1), fmaxf(sc2, sc3));                              \
+        const float sc_lo = fminf(fminf(sc0, sc1), fminf(sc2, sc3));                              \
+        bool pass[2];                                                                             \
+        _Pragma("unroll") for (int nb = 0; nb < 2; ++nb) {                                        \
+            int m = acc[0][nb][0];                                                                \
+            _Pragma("unroll") for (int rb = 0; rb < 8; ++rb)                                      \
+                _Pragma("unroll") for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m; \
+            pass[nb] = ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];                \
+        }                                                                                         \
+        _Pragma("unroll") for (int nb = 0; nb < 2; ++nb) {                                        \
+            uint64_t m = __ballot(pass[nb]);                                                      \
+            while (m) {                                                                           \
+                const uint32_t room = STG - scnt;                                                 \
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),              \
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)); \
+                const bool sel = ((m >> lane) & 1ull) && rank < room;                             \
+                if (sel) {                                                                        \
+                    const uint32_t e = scnt + rank;                                               \
+                    _Pragma("unroll") for (int rb = 0; rb < 8; ++rb)                              \
+                        ds_st128(lds_addr(&stg_v[w][e][rb * 4]), acc[rb][nb]);                    \
+                    const i32x4v_t mt = {(int)(rt_e * BM + 4 * (lane >> 4)), nb * 16 + (lane & 15), \
+                                         __float_as_int(tau[nb]), __float_as_int(sbq[nb])};       \
+                    ds_st128(lds_addr(&stg_m[w][e][0]), mt);                                      \
+                }                                                                                 \
+                const uint64_t took = __ballot(sel);                                              \
+                m &= ~took;                                                                       \
+                scnt += (uint32_t)__builtin_popcountll(took);                                     \
+                if (scnt == STG) BSR_QS16K_DRAIN(STORED);                                         \
+            }                                                                                     \
+        }                                                                                         \
+        if (scnt) BSR_QS16K_DRAIN(STORED);                                                        \
+    } while (0)
+
+    // loop positions x = t * NK + kt; group A works on slices x < JA, group B on x - L for
+    // L <= x < X.  A's tile epilogue at kt == 0 (t > 0), B's at kt == L (t > 0).
+    uint32_t uA = 0, uB = 0;  // the tile each group is on
+    if (grp == 0 && my_rt) load_scales(0);
+    // one slice at loop position x = t * NK + kt (kt a constant once unrolled; a macro, not a
+    // lambda: the fragment arrays must not escape into memory before unrolling)
+#define BSR_QS16K_SLICE(T, KT)                                                                   \
+    do {                                                                                         \
+        const uint32_t x = (T) * NK + (KT);                                                      \
+        _Pragma("unroll") for (int rb = 0; rb < 8; ++rb) {                                        \
+            _Pragma("unroll") for (int nb = 0; nb < 2; ++nb) acc[rb][nb] =                        \
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][KT], acc[rb][nb], 0, 0, 0); \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            if (rb < 4) read_frag(x, rb + 4);                                                    \
+            else read_frag(x + 1, rb - 4);                                                       \
+            if (((KT) & 1) ? rb == 6 : rb == 1) issue_dma(x + A);                                \
+            if (((KT) & 1) && rb == 5) qs_wait<2>();                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+        }                                                                                        \
+    } while (0)
+    // Branch-free slices (a branch around the MFMAs or reads would make the compiler wait for
+    // every LDS read at each join): a group's MFMAs outside its own tiles run on stale
+    // fragments into accumulators that are zeroed (B before its first tile) or no longer
+    // read (A after its last epilogue).
+    for (uint32_t t = 0; t < my_rt; ++t) {
+        // group A's tile epilogue at kt == 0, group B's at kt == L (outside the unrolled
+        // slice loops)
+        if (grp == 0 && t > 0) {
+            bool stored = false;
+            BSR_QS16K_EPILOGUE(uA, stored);
+            zero_acc();
+            ++uA;
+            load_scales(uA);
+            if (stored) wait_vm0();  // global stores / atomics count in vmcnt
+        }
+#pragma unroll
+        for (int kt = 0; kt < L; ++kt) BSR_QS16K_SLICE(t, kt);
+        if (grp == 1) {
+            bool stored = false;
+            if (t > 0) {
+                BSR_QS16K_EPILOGUE(uB, stored);
+                ++uB;
+            }
+            zero_acc();
+            load_scales(uB);
+            if (stored) wait_vm0();
+        }
+#pragma unroll
+        for (int kt = L; kt < NK; ++kt) BSR_QS16K_SLICE(t, kt);
+    }
+    if (my_rt) {
+        // the last half period: group A's last epilogue, group B's last L slices
+        if (grp == 0) {
+            bool stored = false;
+            BSR_QS16K_EPILOGUE(uA, stored);
+            if (stored) wait_vm0();
+        }
+#pragma unroll
+        for (int kt = 0; kt < L; ++kt) BSR_QS16K_SLICE(my_rt, kt);
+    }
+#undef BSR_QS16K_SLICE
+    bool stored = false;
+    if (grp == 1 && my_rt) BSR_QS16K_EPILOGUE(uB, stored);  // group B's last tile
+    (void)stored;
+#undef BSR_QS16K_EPILOGUE
+#undef zero_acc
+#undef load_scales
+#undef BSR_QS16K_DRAIN
+    wait_vm0();
+    wave_lds_order();
     flush_keys();
 }
 
