@@ -445,11 +445,15 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         return skinny ? launch_filter_skinny_emit(g, ix->stream, e0, e1)
                       : launch_filter_emit(ix->op, g, ix->stream, e0, e1);
     }));
-    ev_begin(ix, ix->ev_select);
-    BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(), kp,
-                               ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(), ix->tau_excl.as<float>(),
-                               status, ix->stream));
-    ev_end(ix, ix->ev_select);
+    // lists of <= 1024 keys (k <= 10): the rescore kernel selects its own k' candidates
+    const bool fused_select = cap <= kFusedSelectCap;
+    if (!fused_select) {
+        ev_begin(ix, ix->ev_select);
+        BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(),
+                                   kp, ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(),
+                                   ix->tau_excl.as<float>(), status, ix->stream));
+        ev_end(ix, ix->ev_select);
+    }
     ev_begin(ix, ix->ev_rescore);
     RescoreArgs ra{};
     ra.rows = ix->rows.as<float>();
@@ -468,12 +472,20 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     ra.out_keys = ix->keys.as<uint64_t>();
     ra.fail_cnt = status + kStFail;
     ra.fail_list = ix->fail.as<uint32_t>();
+    if (fused_select) {
+        ra.sel = 1;
+        ra.cand_keys = ix->cand.as<uint64_t>();
+        ra.cnt = ix->cnt.as<uint32_t>();
+        ra.cap = cap;
+        ra.tau0 = ix->tau.as<float>();
+    }
     BSR_HIP(launch_rescore(ra, ix->stream));
     // Second chance, in the same stream (and graph): a query that failed certification is
     // rescored over EVERY row it emitted (~4k'), certified against tau0 -- far less than a
     // scan.  The failed count is read on the device, so no host round trip; what fails here
     // too goes to fail2 (exact scan, host-driven).
     RescoreArgs rb = ra;
+    rb.sel = 0;
     rb.n_items = nq;
     rb.n_items_dev = status + kStFail;
     rb.qlist = ix->fail.as<uint32_t>();

@@ -100,11 +100,105 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             for (uint32_t c = threadIdx.x; c < a.ld; c += 64 * W) ldq_all[c] = a.qf32[(uint64_t)q * a.ld + c];
         if constexpr (W > 1) __syncthreads();
         else wave_sync();
-        // mode B (every emitted candidate) or mode A (the k' selected ones)
-        const bool all = a.cand_keys != nullptr;
-        const uint32_t cnt = all ? a.cnt[q] : a.ncand[q];
-        const bool overflow = all && cnt > a.cap;  // rows were dropped: nothing can be certified
-        const uint32_t c = overflow ? 0u : cnt;
+        // mode S (a.sel: select the k' candidates here, from the emitted keys), mode B (every
+        // emitted candidate) or mode A (the k' selected ones, from k_select_cand)
+        const bool sel = W == 1 && a.sel;
+        const bool all = !sel && a.cand_keys != nullptr;
+        const uint32_t cnt = (sel || all) ? a.cnt[q] : a.ncand[q];
+        const bool overflow = (sel || all) && cnt > a.cap;  // rows were dropped: nothing can be certified
+        uint32_t c = overflow ? 0u : cnt;
+        float tx_sel = INFINITY;
+        uint32_t sel_row = 0;
+        if (W == 1 && sel) {
+            // the (kp+1)-th smallest key T by radix select over the emitted keys (cap <= 1024:
+            // 16 registers), the kp keys below it compacted through LDS; kp <= 63 (one pass)
+            constexpr int NR = 16;
+            const uint64_t* src = a.cand_keys + (uint64_t)q * a.cap;
+            uint64_t x[NR];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const uint32_t i = j * kWave + lane;
+                x[j] = i < c ? src[i] : kKeyNone;
+            }
+            uint64_t T = kKeyNone;
+            if (!overflow && c > a.kp) {
+                // the high words first (score bits: only the bits below the highest one in which
+                // the emitted keys differ are searched), then -- only when several keys share
+                // the K-th high word -- the low words (rows) among those
+                const uint32_t K = a.kp + 1;
+                uint32_t hmin = ~0u, hmax = 0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j)
+                    if (x[j] != kKeyNone) {
+                        hmin = min(hmin, (uint32_t)(x[j] >> 32));
+                        hmax = max(hmax, (uint32_t)(x[j] >> 32));
+                    }
+                for (int off = 32; off > 0; off >>= 1) {
+                    hmin = min(hmin, (uint32_t)__shfl_xor((int)hmin, off, kWave));
+                    hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off, kWave));
+                }
+                const uint32_t diff = hmin ^ hmax;
+                const int top = diff ? 31 - __builtin_clz(diff) : -1;
+                // (top < 0: every key has the same high word)
+                uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
+                for (int b = top; b >= 0; --b) {
+                    const uint32_t t = Th | (1u << b);
+                    uint32_t below = 0;
+#pragma unroll
+                    for (int j = 0; j < NR; ++j)
+                        if (j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
+                    if (below < K) Th = t;
+                }
+                uint32_t lt = 0, eq = 0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j)
+                    if (j * kWave < (int)c) {
+                        const uint32_t h = (uint32_t)(x[j] >> 32);
+                        lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
+                        eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
+                    }
+                const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
+                uint32_t Tl = 0;
+                if (eq > 1)
+                    for (int b = 31; b >= 0; --b) {
+                        const uint32_t t = Tl | (1u << b);
+                        uint32_t below = 0;
+#pragma unroll
+                        for (int j = 0; j < NR; ++j)
+                            if (j * kWave < (int)c)
+                                below += (uint32_t)__popcll(
+                                    __ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
+                        if (below < K2) Tl = t;
+                    }
+                else
+#pragma unroll
+                    for (int j = 0; j < NR; ++j) {  // the one key with high word Th
+                        const uint64_t m = __ballot(x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th);
+                        if (m) Tl = (uint32_t)__shfl((int)(uint32_t)x[j], __builtin_ctzll(m), kWave);
+                    }
+                T = ((uint64_t)Th << 32) | Tl;
+                tx_sel = score_key_score(T);
+                c = a.kp;
+            } else if (!overflow) {
+                tx_sel = a.tau0[q];  // every emitted row is a candidate; tau0 bounds the rest
+            }
+            uint32_t* const lsel = reinterpret_cast<uint32_t*>(lds);
+            uint32_t base = 0;
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const bool pick = x[j] < T;
+                const uint64_t m = __ballot(pick);
+                if (pick) {
+                    const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    lsel[pos] = key_row(x[j]);
+                }
+                base += (uint32_t)__popcll(m);
+            }
+            wave_sync();
+            sel_row = lane < (int)c ? lsel[lane] : 0u;
+            wave_sync();
+        }
         const float mag_b = a.nb[q];
         const uint32_t ld = a.ld, dim = a.dim, nch = ld / 64;
         const float* rows = a.rows;
@@ -122,7 +216,8 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             const uint32_t nchk = NC ? NC : nch;
             for (uint32_t base = 64 * w; base < c; base += 64 * W) {
                 const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
-                const uint32_t myrow = all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc])
+                const uint32_t myrow = sel ? sel_row
+                                     : all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc])
                                            : a.cand_rows[(uint64_t)q * a.kp + cc];
                 float acc[1] = {-0.0f}, mx[1] = {0.0f};
                 uint32_t lrow[16];
@@ -198,7 +293,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                 // lie strictly below that, and no excluded row can be element-wise identical to
                 // the query.  Mode B: every emitted row is a candidate, so tau_x is the
                 // emission threshold tau0.
-                const float tx = overflow ? INFINITY : (all ? a.tau0[q] : a.tau_excl[q]);
+                const float tx = overflow ? INFINITY : sel ? tx_sel : (all ? a.tau0[q] : a.tau_excl[q]);
                 const double ebound = (double)a.ebound[q];
                 bool ok;
                 if (tx == -INFINITY) {

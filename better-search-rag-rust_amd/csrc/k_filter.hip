@@ -1011,71 +1011,6 @@ __global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__
     }
 }
 
-// The same selection for lists of at most 64 * NR keys (k <= 10: cap = 1024), by radix
-// select instead of a sorted list: the keys stay in registers, and the (kp+1)-th smallest
-// key T is built bit by bit from the top (count of keys below a trial value: one ballot +
-// popcount per register), then the kp keys below T are compacted (ballot + mbcnt).  The
-// candidate order differs from k_select_cand's (the rescore does not depend on it); the set
-// and tau_excl are the same.  One wave per query.
-template <int NR>
-__global__ __launch_bounds__(64) void k_select_cand_radix(const uint64_t* __restrict__ cand,
-                                                          const uint32_t* __restrict__ cnt, uint32_t cap,
-                                                          uint32_t nq, const float* __restrict__ tau,
-                                                          uint32_t kp, uint32_t* __restrict__ cand_rows,
-                                                          uint32_t* __restrict__ ncand,
-                                                          float* __restrict__ tau_excl,
-                                                          uint32_t* __restrict__ status) {
-    const uint32_t q = blockIdx.x;
-    if (q >= nq) return;
-    const int lane = threadIdx.x;
-    const uint32_t c = cnt[q];
-    if (c > cap) {  // overflow: rows were dropped, nothing can be certified
-        if (lane == 0) { ncand[q] = 0; tau_excl[q] = INFINITY; }
-        return;
-    }
-    const uint64_t* src = cand + (uint64_t)q * cap;
-    uint64_t x[NR];
-    // registers past the emitted count hold kKeyNone and are skipped (uniform: j * 64 >= c)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-        const uint32_t i = j * kWave + lane;
-        x[j] = i < c ? src[i] : kKeyNone;
-    }
-    uint32_t* out = cand_rows + (uint64_t)q * kp;
-    if (c <= kp) {  // every emitted row is a candidate; tau0 bounds the rest
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const uint32_t i = j * kWave + lane;
-            if (i < c) out[i] = key_row(x[j]);
-        }
-        if (lane == 0) { ncand[q] = c; tau_excl[q] = tau[q]; }
-        return;
-    }
-    // T = the (kp+1)-th smallest key: the largest t with #(keys < t) < kp + 1
-    uint64_t T = 0;
-    for (int b = 63; b >= 0; --b) {
-        const uint64_t t = T | (1ull << b);
-        uint32_t below = 0;
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-            if (j * kWave < (int)c) below += (uint32_t)__popcll(__ballot(x[j] < t));
-        if (below < kp + 1) T = t;
-    }
-    uint32_t base = 0;
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-        const bool sel = x[j] < T;
-        const uint64_t m = __ballot(sel);
-        if (sel) {
-            const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            out[pos] = key_row(x[j]);
-        }
-        base += (uint32_t)__popcll(m);
-    }
-    if (lane == 0) { ncand[q] = kp; tau_excl[q] = score_key_score(T); }
-}
-
 // ------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------
@@ -1158,17 +1093,6 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,
                               const float* tau, uint32_t kp, uint32_t* cand_rows, uint32_t* ncand,
                               float* tau_excl, uint32_t* status, hipStream_t s) {
-    if (cap <= 16 * kWave) {  // k <= 10: radix select with the keys in registers
-        const uint32_t nr = (cap + kWave - 1) / kWave;
-#define BSR_RADIX(NR)                                                                                      \
-    hipLaunchKernelGGL(k_select_cand_radix<NR>, dim3(nq), dim3(64), 0, s, cand, cnt, cap, nq, tau, kp,     \
-                       cand_rows, ncand, tau_excl, status)
-        if (nr <= 4) BSR_RADIX(4);
-        else if (nr <= 8) BSR_RADIX(8);
-        else BSR_RADIX(16);
-#undef BSR_RADIX
-        return hipGetLastError();
-    }
     const uint32_t e = (kp + 1 + 63) / 64;
 #define BSR_SELECT(E)                                                                                   \
     hipLaunchKernelGGL(k_select_cand<E>, dim3(nq), dim3(64), 0, s, cand, cnt, cap, nq, tau, kp, cand_rows, \

@@ -143,6 +143,10 @@ struct RescoreArgs {
     const uint32_t* cnt;
     uint32_t cap;
     const float* tau0;
+    // mode S (sel != 0, one-wave launch, cap <= 1024): the k' candidates selected in the
+    // rescore kernel itself from cand_keys / cnt (radix select; tau_x = the (k'+1)-th score,
+    // or tau0 when fewer were emitted) -- k_select_cand is not launched
+    uint32_t sel;
     uint32_t k;
     const float* ebound;        // per-query certification bound E_q
     uint64_t* out_keys;         // [nq][k]
@@ -151,6 +155,8 @@ struct RescoreArgs {
 };
 // Workgroups of the device-counted rescore (failed certifications, usually a few queries).
 constexpr uint32_t kRescoreAllGrid = 128;
+// Candidate lists up to this many keys (k <= 10) are selected inside the rescore kernel.
+constexpr uint32_t kFusedSelectCap = 1024;
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s);
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold
 // grid * kScanQF * k keys.

@@ -408,7 +408,9 @@ def test_profile_levels(bsr_mod, oracle_mod, gpu):
         ix.profile(reset=True)
         _assert_same(ix.local_top_k(qs, 10), want, f"level {level}")
         seen[level] = ix.profile(reset=True)
-    assert seen[2].gemm_emit_launches == 1 and seen[2].select_launches == 1 and seen[2].searches == 1
+    # k = 10: the candidate selection runs inside the rescore kernel (no select launch)
+    assert seen[2].gemm_emit_launches == 1 and seen[2].select_launches == 0 and seen[2].searches == 1
+    assert seen[2].rescore_launches == 1
     assert seen[1].gemm_emit_launches == 1 and seen[1].select_launches == 0 and seen[1].searches == 0
     assert seen[1].gemm_emit_ms > 0.0
     assert seen[0].gemm_emit_launches == 0 and seen[0].searches == 0
