@@ -916,13 +916,14 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
 // so that about ks * stride rows of the shard or more reach it.  4 waves per query.  Also
 // zeroes the query's candidate counter and (block 0) the emit status words.
 // ------------------------------------------------------------------------------------
+template <int E>  // ks <= 64 E
 __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S, uint32_t s_ld,
                                                     uint32_t n_s, uint32_t nq, uint32_t qpad,
                                                     const uint32_t* __restrict__ qflags,
                                                     uint32_t ks, float* __restrict__ tau,
                                                     uint32_t* __restrict__ cnt,
                                                     uint32_t* __restrict__ status) {
-    __shared__ uint64_t part[4][64];
+    __shared__ uint64_t part[4][64 * E];
     const uint32_t q = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
@@ -936,34 +937,61 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
         if (t == 0) tau[q] = -INFINITY;
         return;
     }
-    // wave w streams a quarter of the values, keeping its ks best
-    WaveTopK<1> L;
-    L.init();
-    uint64_t thr = kKeyNone;
+    // wave w takes a quarter of the values.  Pass 1: each lane's maximum; the wave's ks-th
+    // largest lane maximum is a lower bound lb_w of the query's ks-th largest value (those ks
+    // maxima are ks distinct values), and lb = max_w lb_w.  Pass 2 (L2-hot re-read): only
+    // values >= lb are offered to the wave's ks best -- a few per wave instead of streaming
+    // every batch through the sorted list.
+    __shared__ float lbw[4];
     const float* s = S + (uint64_t)q * s_ld;
     const uint32_t per = (n_s + 3) / 4, lo = w * per, hi = lo + per < n_s ? lo + per : n_s;
-    // 16 loads per lane in flight, then their offers (most return after one ballot)
-    constexpr int B = 16;
+    constexpr int B = 16;  // loads per lane in flight
+    float m = -INFINITY;
     for (uint32_t base = lo; base < hi; base += B * kWave) {
         float v[B];
 #pragma unroll
         for (int j = 0; j < B; ++j) {
             const uint32_t i = base + j * kWave + lane;
-            v[j] = i < hi ? s[i] : 0.0f;
+            v[j] = i < hi ? s[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) m = fmaxf(m, v[j]);
+    }
+    if (ks <= (uint32_t)kWave) {
+        const uint64_t sorted = wave_sort64(score_key(m, (uint32_t)lane));  // ascending key = descending score
+        const uint64_t kth = shfl64(sorted, (int)ks - 1);
+        if (lane == 0) lbw[w] = score_key_score(kth);
+    } else if (lane == 0) {
+        lbw[w] = -INFINITY;  // (more than 64 needed: no lower bound from 64 lane maxima)
+    }
+    __syncthreads();
+    const float lb = fmaxf(fmaxf(lbw[0], lbw[1]), fmaxf(lbw[2], lbw[3]));
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    for (uint32_t base = lo; base < hi; base += B * kWave) {
+        float v[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const uint32_t i = base + j * kWave + lane;
+            v[j] = i < hi ? s[i] : -INFINITY;
         }
 #pragma unroll
         for (int j = 0; j < B; ++j) {
             const uint32_t i = base + j * kWave + lane;
-            L.offer(i < hi ? score_key(v[j], i) : kKeyNone, (int)ks, thr);
+            L.offer(v[j] >= lb ? score_key(v[j], i) : kKeyNone, (int)ks, thr);
         }
     }
-    part[w][lane] = L.v[0];
+#pragma unroll
+    for (int e = 0; e < E; ++e) part[w][e * 64 + lane] = L.v[e];
     __syncthreads();
     if (w == 0) {
-        WaveTopK<1> M;
+        WaveTopK<E> M;
         M.init();
         uint64_t mt = kKeyNone;
-        for (int src = 0; src < 4; ++src) M.offer(part[src][lane], (int)ks, mt);
+        for (int src = 0; src < 4; ++src)
+#pragma unroll
+            for (int e = 0; e < E; ++e) M.offer(part[src][e * 64 + lane], (int)ks, mt);
         if (lane == 0) tau[q] = score_key_score(mt);
     }
 }
@@ -1086,8 +1114,13 @@ hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hip
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
                              hipStream_t s) {
-    hipLaunchKernelGGL(k_select_tau, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau, cnt,
-                       status);
+    if (ks > 2 * kWave) return hipErrorInvalidValue;
+    if (ks > kWave)
+        hipLaunchKernelGGL(k_select_tau<2>, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau,
+                           cnt, status);
+    else
+        hipLaunchKernelGGL(k_select_tau<1>, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau,
+                           cnt, status);
     return hipGetLastError();
 }
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,
