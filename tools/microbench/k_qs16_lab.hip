@@ -18,7 +18,8 @@
 // 4 = staged entries scored later, one step (2 entries) per slice inside the next tile's
 // MFMA stream (the two waves of a SIMD at different groups) instead of in the epilogue;
 // 8 = one barrier per FOUR slices (12-slot ring, 8 slices ahead; NK % 4 == 0);
-// 16 = timing probe: the final key-ring flush (global atomics + stores) skipped.
+// 16 = timing probe: the final key-ring flush (global atomics + stores) skipped;
+// 32 = fragment reads as inline asm with hand-counted lgkmcnt waits.
 // Included after the product k_filter.hip (uses its types and helpers).
 namespace bsrlab {
 using namespace bsr;
@@ -161,8 +162,20 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16s(GemmArgs p) {
     };
     const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
     i32x4v_t fa[4];
+    // VAR & 32: fragment reads as inline asm with hand-counted waits (the compiler does not
+    // track them, so a branch in the loop does not make it wait for every read at the join)
     auto read_frag = [&](uint32_t jj, int rb) {
-        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
+        if constexpr ((VAR & 32) != 0) {
+            const uint32_t addr = lds_addr(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
+            asm volatile("ds_read_b128 %0, %1" : "=v"(fa[rb & 3]) : "v"(addr) : "memory");
+        } else {
+            fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
+        }
+    };
+    // before the MFMAs of row block rb: its read (issued four blocks earlier) has returned
+    // (LDS returns in order; at most the three younger reads still in flight)
+    auto frag_wait = [&](int rb) {
+        if constexpr ((VAR & 32) != 0) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(fa[rb & 3]));
     };
 
     i32x4v_t acc[8][2];
@@ -232,6 +245,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16s(GemmArgs p) {
             const bool bar_slice = (kt % BAR) == BAR - 1;
 #pragma unroll
             for (int rb = 0; rb < 8; ++rb) {
+                frag_wait(rb);
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
                     if (kt == 0) {
