@@ -126,7 +126,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap, timing, host transport
+        # (gloo prints its connection report to stdout: keep stdout for the one JSON line)
+        sys.stdout.flush()
+        saved_fd = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap, timing, host transport
+        finally:
+            os.dup2(saved_fd, 1)
+            os.close(saved_fd)
     ndev = torch.cuda.device_count()
     device = local_rank % max(ndev, 1)
     torch.cuda.set_device(device)

@@ -2,6 +2,7 @@
 // communicator, gather (src/mpi_helpers/metrics.rs:56-138), the host merge
 // (:141-171) and the composed parallel search (:174-206).
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -38,6 +39,43 @@ int bsr_copy_out_impl(bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx,
         return set_error(BSR_E_INVALID, "internal error (exception)");         \
     }
 
+// Host memory for the gathered lists that grows on demand: pinned when a HIP device is
+// present (the RCCL path copies into it; pageable vectors would make those copies staged and
+// synchronous), plain memory otherwise (a host-transport communicator on a CPU-only node).
+template <class T>
+struct PinnedVec {
+    T* p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec&) = delete;
+    PinnedVec& operator=(const PinnedVec&) = delete;
+    ~PinnedVec() { release(); }
+    void release() {
+        if (p && pinned) (void)hipHostFree(p);
+        else free(p);
+        p = nullptr;
+        cap = 0;
+    }
+    int resize(size_t n) {
+        if (n <= cap) return BSR_OK;
+        release();
+        const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        void* q = nullptr;
+        pinned = hipHostMalloc(&q, bytes, hipHostMallocDefault) == hipSuccess;
+        if (!pinned) {
+            (void)hipGetLastError();  // (no device: clear the sticky error)
+            q = malloc(bytes);
+        }
+        if (!q) return set_error(BSR_E_NOMEM, "host allocation of %zu bytes failed", bytes);
+        p = static_cast<T*>(q);
+        cap = n;
+        return BSR_OK;
+    }
+    T* data() { return p; }
+    const T* data() const { return p; }
+};
+
 // The rank group of the exchange step: RCCL over xGMI (one GPU per rank), or a host
 // transport given by the caller (bsr_comm_init_host: e.g. gloo/MPI stand-ins on CPU).
 struct bsr_comm {
@@ -47,9 +85,9 @@ struct bsr_comm {
     bsr_host_allgather_fn host_fn = nullptr;  // non-null: host transport
     void* host_user = nullptr;
     DevBuf send_idx, send_dist, send_cnt, recv_idx, recv_dist, recv_cnt;
-    std::vector<uint64_t> h_idx;   // root: gathered [size][nq][k]
-    std::vector<float> h_dist;
-    std::vector<uint32_t> h_cnt;   // root: [size][nq]
+    PinnedVec<uint64_t> h_idx;     // root: gathered [size][nq][k]
+    PinnedVec<float> h_dist;
+    PinnedVec<uint32_t> h_cnt;     // root: [size][nq]
     std::vector<uint8_t> h_send, h_recv;  // host transport packing
     std::vector<uint64_t> m_idx;   // root merge output staging (device outputs)
     std::vector<float> m_dist;
@@ -304,9 +342,9 @@ static int exchange_lists(bsr_comm* c, const uint64_t* idx, const float* dist, c
         if (c->host_fn(c->h_send.data(), c->h_recv.data(), bytes, c->host_user) != 0)
             return set_error(BSR_E_RCCL, "host all-gather callback failed");
         if (root) {
-            c->h_cnt.resize((size_t)nq * P);
-            c->h_dist.resize(nk * P);
-            c->h_idx.resize(nk * P);
+            BSR_TRY(c->h_cnt.resize((size_t)nq * P));
+            BSR_TRY(c->h_dist.resize(nk * P));
+            BSR_TRY(c->h_idx.resize(nk * P));
             for (size_t r = 0; r < P; ++r) {
                 const uint8_t* m = c->h_recv.data() + r * bytes;
                 memcpy(c->h_cnt.data() + r * nq, m, (size_t)nq * 4);
@@ -344,9 +382,9 @@ static int exchange_lists(bsr_comm* c, const uint64_t* idx, const float* dist, c
     BSR_NCCL(ncclAllGather(s_cnt, c->recv_cnt.p, (size_t)nq * sizeof(uint32_t), ncclUint8, c->comm, stream));
     BSR_NCCL(ncclGroupEnd());
     if (root) {
-        c->h_idx.resize(nk * P);
-        c->h_dist.resize(nk * P);
-        c->h_cnt.resize((size_t)nq * P);
+        BSR_TRY(c->h_idx.resize(nk * P));
+        BSR_TRY(c->h_dist.resize(nk * P));
+        BSR_TRY(c->h_cnt.resize((size_t)nq * P));
         BSR_HIP(hipMemcpyAsync(c->h_idx.data(), c->recv_idx.p, nk * P * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         BSR_HIP(hipMemcpyAsync(c->h_dist.data(), c->recv_dist.p, nk * P * sizeof(float), hipMemcpyDeviceToHost, stream));
         BSR_HIP(hipMemcpyAsync(c->h_cnt.data(), c->recv_cnt.p, (size_t)nq * P * sizeof(uint32_t), hipMemcpyDeviceToHost,
