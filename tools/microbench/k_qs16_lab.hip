@@ -453,6 +453,12 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16k(GemmArgs args) {
     };
 
     i32x4v_t acc[8][2];
+#define mask_acc(M)                                                                               \
+    do {                                                                                          \
+        const int m_ = __builtin_amdgcn_readfirstlane(M);                                         \
+        _Pragma("unroll") for (int rb = 0; rb < 8; ++rb)                                          \
+            _Pragma("unroll") for (int nb = 0; nb < 2; ++nb) acc[rb][nb] &= m_;                   \
+    } while (0)
 #define zero_acc()                                                                                \
     do {                                                                                          \
         _Pragma("unroll") for (int rb = 0; rb < 8; ++rb)                                          \
@@ -574,11 +580,13 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16k(GemmArgs args) {
         if (grp == 0 && t > 0) {
             bool stored = false;
             BSR_QS16K_EPILOGUE(uA, stored);
-            zero_acc();
             ++uA;
             load_scales(uA);
             if (stored) wait_vm0();  // global stores / atomics count in vmcnt
         }
+        // accumulators zeroed without a branch (AND with a wave-uniform mask): a conditional
+        // assignment would split their live ranges and cost register copies in the loop
+        mask_acc((grp == 0 && t > 0) ? 0 : -1);
 #pragma unroll
         for (int kt = 0; kt < L; ++kt) BSR_QS16K_SLICE(t, kt);
         if (grp == 1) {
@@ -587,10 +595,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16k(GemmArgs args) {
                 BSR_QS16K_EPILOGUE(uB, stored);
                 ++uB;
             }
-            zero_acc();
             load_scales(uB);
             if (stored) wait_vm0();
         }
+        mask_acc(grp == 1 ? 0 : -1);
 #pragma unroll
         for (int kt = L; kt < NK; ++kt) BSR_QS16K_SLICE(t, kt);
     }
@@ -610,6 +618,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16k(GemmArgs args) {
     (void)stored;
 #undef BSR_QS16K_EPILOGUE
 #undef zero_acc
+#undef mask_acc
 #undef load_scales
 #undef BSR_QS16K_DRAIN
     wait_vm0();

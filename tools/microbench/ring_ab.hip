@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
     std::vector<V> vs = {
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, {}, 8},
         {"qs16 staged (lab)", bsrlab::k_filter_qs16s<12, 0>, {}, 8},
+        {"skewed groups (lab)", bsrlab::k_filter_qs16k<12>, {}, 8},
         {"level-1 only", bsrlab::k_filter_qs16s<12, 1>, {}, 8},
         {"qs8 (round 1)", bsrlab::k_filter_qs8<true, 12, false, 72>, {}, 8},
     };
@@ -98,7 +99,7 @@ int main(int argc, char** argv) {
         return ms;
     };
     // ---- cross-check: emitted candidate sets and sample scores
-    const int n_check = 2;  // product + the staged variants (emitting)
+    const int n_check = 3;  // product + the staged variants (emitting)
     std::vector<std::vector<uint64_t>> sets(n_check);
     for (int i = 0; i < n_check; ++i) {
         run(vs[i].k, g, tau_emit, vs[i].nw);
