@@ -451,7 +451,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         ev_begin(ix, ix->ev_select);
         BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(),
                                    kp, ix->cand_rows.as<uint32_t>(), ix->ncand.as<uint32_t>(),
-                                   ix->tau_excl.as<float>(), status, ix->stream));
+                                   ix->tau_excl.as<float>(), ix->stream));
         ev_end(ix, ix->ev_select);
     }
     ev_begin(ix, ix->ev_rescore);

@@ -1004,8 +1004,7 @@ __global__ __launch_bounds__(64) void k_select_cand(const uint64_t* __restrict__
                                                     uint32_t nq, const float* __restrict__ tau,
                                                     uint32_t kp, uint32_t* __restrict__ cand_rows,
                                                     uint32_t* __restrict__ ncand,
-                                                    float* __restrict__ tau_excl,
-                                                    uint32_t* __restrict__ status) {
+                                                    float* __restrict__ tau_excl) {
     const uint32_t q = blockIdx.x;
     if (q >= nq) return;
     const uint32_t c = cnt[q];
@@ -1125,11 +1124,11 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
 }
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,
                               const float* tau, uint32_t kp, uint32_t* cand_rows, uint32_t* ncand,
-                              float* tau_excl, uint32_t* status, hipStream_t s) {
+                              float* tau_excl, hipStream_t s) {
     const uint32_t e = (kp + 1 + 63) / 64;
 #define BSR_SELECT(E)                                                                                   \
     hipLaunchKernelGGL(k_select_cand<E>, dim3(nq), dim3(64), 0, s, cand, cnt, cap, nq, tau, kp, cand_rows, \
-                       ncand, tau_excl, status)
+                       ncand, tau_excl)
     switch (e) {
         case 1: BSR_SELECT(1); break;
         case 2: BSR_SELECT(2); break;

@@ -110,18 +110,20 @@ constexpr uint32_t kSkinnyMaxQ = 16;
 hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
-// tau[q] = the ks-th best sampled score; also zeroes cnt[0..qpad) and the status words
-// kStFail / kStEmitted for the emit pass that follows.
+// tau[q] = the ks-th best sampled score (ks <= 128); also zeroes cnt[0..qpad) and the status
+// words kStFail / kStEmitted / kStFail2 for the emit pass and rescores that follow.
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq,
                              uint32_t qpad, const uint32_t* qflags, uint32_t ks, float* tau,
                              uint32_t* cnt, uint32_t* status, hipStream_t s);
+// The k' = kp best emitted candidates (rows) and tau_excl = the (kp+1)-th score, for lists
+// larger than kFusedSelectCap (smaller ones are selected inside the rescore).
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap,
                               uint32_t nq, const float* tau, uint32_t kp, uint32_t* cand_rows,
-                              uint32_t* ncand, float* tau_excl, uint32_t* status,
-                              hipStream_t s);
+                              uint32_t* ncand, float* tau_excl, hipStream_t s);
 
 // ---- exact arithmetic (k_exact.hip) ---------------------------------------------------
-// Exact rescoring of candidates + certification, one wave per listed query.
+// Exact rescoring of candidates + certification (one wave per query, or device-counted
+// 8-wave workgroups for the second chance).
 struct RescoreArgs {
     const float* rows;          // f32 [n_pad][ld]
     uint32_t ld, dim;
