@@ -47,6 +47,7 @@ struct DevBuf {
 };
 
 bool is_device_ptr(const void* p);
+hipError_t stream_wait(hipStream_t s);  // poll until the stream's work is done
 int select_device(int device);
 
 static inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }

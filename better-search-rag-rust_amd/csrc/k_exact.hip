@@ -504,6 +504,95 @@ __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint3
     if (i == 0) out_count[q] = cnt;
 }
 
+// The root's merge (compute_global_top_k, src/mpi_helpers/metrics.rs:141-171) of gathered
+// lists laid out [P][nq][k_in] (counts [P][nq]) on the device, one wave per query: the
+// rank-order concatenation is staged in LDS with its order key (distance, position in the
+// concatenation) -- the stable sort by distance is the ascending order of that key; -0.0
+// and +0.0 compare equal as partial_cmp has them -- every entry whose index occurs at a
+// smaller key is dropped (the HashSet keeps first occurrences), and the k smallest keys left
+// are the result.  Rows past out_count[q] are (~0, +inf), as merge_top_k_lists writes them.
+// A NaN distance: out_count[q] = 0 and the lowest such q in *first_nan (the reference panics).
+template <int E>
+__global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__ idx,
+                                                    const float* __restrict__ dist,
+                                                    const uint32_t* __restrict__ cnt, uint32_t P,
+                                                    uint32_t nq, uint32_t k_in, uint32_t k,
+                                                    uint64_t* __restrict__ out_idx,
+                                                    float* __restrict__ out_dist,
+                                                    uint32_t* __restrict__ out_count,
+                                                    uint32_t* __restrict__ first_nan) {
+    __shared__ uint64_t s_idx[kMergeMaxEntries];
+    __shared__ uint64_t s_key[kMergeMaxEntries];
+    __shared__ float s_dist[kMergeMaxEntries];
+    const uint32_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (q >= nq) return;
+    // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
+    const uint32_t c_l = lane < (int)P ? min(cnt[(uint64_t)lane * nq + q], k_in) : 0u;
+    uint32_t incl = c_l;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, off, kWave);
+        if (lane >= off) incl += t;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t off_l = incl - c_l;
+    bool nan = false;
+    for (uint32_t l = 0; l < P; ++l) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, (int)l);
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)l);
+        const uint64_t base = ((uint64_t)l * nq + q) * k_in;
+        for (uint32_t i = lane; i < c; i += kWave) {
+            const float d = dist[base + i];
+            nan |= d != d;
+            s_idx[o + i] = idx[base + i];
+            s_dist[o + i] = d;
+            s_key[o + i] = ((uint64_t)ord_f32(d + 0.0f) << 32) | (o + i);  // (-0.0 + 0.0 = +0.0)
+        }
+    }
+    __syncthreads();
+    uint64_t* const oi = out_idx + (uint64_t)q * k;
+    float* const od = out_dist + (uint64_t)q * k;
+    if (__ballot(nan)) {
+        if (lane == 0) {
+            out_count[q] = 0;
+            atomicMin(first_nan, q);
+        }
+        for (uint32_t p = lane; p < k; p += kWave) {
+            oi[p] = ~0ull;
+            od[p] = INFINITY;
+        }
+        return;
+    }
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    for (uint32_t b = 0; b < total; b += kWave) {
+        const uint32_t j = b + lane;
+        uint64_t key = kKeyNone;
+        if (j < total) {
+            key = s_key[j];
+            const uint64_t x = s_idx[j];
+            for (uint32_t i = 0; i < total; ++i)  // an earlier-sorting copy of the same index
+                if (s_idx[i] == x && s_key[i] < key) { key = kKeyNone; break; }
+        }
+        L.offer(key, (int)k, thr);
+    }
+    uint32_t got = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t p = e * kWave + lane;
+        const uint64_t key = L.v[e];
+        got += (uint32_t)__popcll(__ballot(p < k && key != kKeyNone));
+        if (p < k) {
+            const uint32_t j = (uint32_t)key;
+            oi[p] = key != kKeyNone ? s_idx[j] : ~0ull;
+            od[p] = key != kKeyNone ? s_dist[j] : INFINITY;
+        }
+    }
+    if (lane == 0) out_count[q] = got;
+}
+
 // src/metrics.rs:143-165 for one pair (single lane, fully sequential, from global memory).
 __global__ void k_cosine_pair(const float* __restrict__ a, uint32_t la, const float* __restrict__ b,
                               uint32_t lb, float* __restrict__ out) {
@@ -603,6 +692,24 @@ hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64
     const uint64_t total = (uint64_t)nq * k;
     hipLaunchKernelGGL(k_finalize, dim3(grid_for(total, 256)), dim3(256), 0, s, keys, nq, k, n, offset,
                        out_idx, out_dist, out_count, status, emit_cnt, cur_status);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_lists(const uint64_t* idx, const float* dist, const uint32_t* cnt, uint32_t P, uint32_t nq,
+                              uint32_t k_in, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count,
+                              uint32_t* first_nan, hipStream_t s) {
+    if (P > (uint32_t)kWave || (uint64_t)P * k_in > kMergeMaxEntries || k > 4 * kWave) return hipErrorInvalidValue;
+    const uint32_t e = (k + 63) / 64;
+#define BSR_MLISTS(E)                                                                                \
+    hipLaunchKernelGGL(k_merge_lists<E>, dim3(nq), dim3(64), 0, s, idx, dist, cnt, P, nq, k_in, k, out_idx, \
+                       out_dist, out_count, first_nan)
+    switch (e) {
+        case 1: BSR_MLISTS(1); break;
+        case 2: BSR_MLISTS(2); break;
+        case 3: BSR_MLISTS(3); break;
+        default: BSR_MLISTS(4); break;
+    }
+#undef BSR_MLISTS
     return hipGetLastError();
 }
 
