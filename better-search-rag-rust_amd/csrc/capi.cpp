@@ -542,7 +542,9 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         ld = reinterpret_cast<const float*>(ix->h_res + ix->res_off_dist);
         lc = reinterpret_cast<const uint32_t*>(ix->h_res + ix->res_off_cnt);
     }
-    const bool dev_merge = !c->host_fn && device_merge_fits((uint32_t)c->size, k, k) && ix->res_bytes;
+    // (the root merges on the device into its own result buffer: only after its own search
+    // succeeded, i.e. that buffer is sized for this batch)
+    const bool dev_merge = !c->host_fn && ok && device_merge_fits((uint32_t)c->size, k, k);
     BSR_TRY(exchange_lists(c, ok ? li : nullptr, ok ? ld : nullptr, ok ? lc : nullptr, !ok, nq, k,
                            c->host_fn ? nullptr : ix->stream, !dev_merge));
     if (ok) bsr_index_collect_profile_impl(ix);

@@ -145,7 +145,9 @@ int bsr_local_top_k(bsr_index* ix, const float* queries, uint32_t n_queries, uin
 /* ---- a-5: compute_global_top_k over n_lists per-rank lists, for n_queries queries.
  * Input list l of query q: idx[(l*n_queries+q)*k_in ..] with count[l*n_queries+q]
  * entries.  Rank-order concatenation + stable sort by distance + dedupe, keep k.
- * Host memory only (the reference merges on rank 0's host). ------------------------- */
+ * Host arrays: merged on the host (threads over queries).  Every array in device memory
+ * (n_lists <= 64, n_lists * k_in <= 1024, k <= 256): merged on the GPU, one wave per query
+ * (the RCCL path's root merge).  Rows past out_count[q] are (~0, +inf). -------------- */
 int bsr_global_top_k(const uint64_t* idx, const float* dist, const uint32_t* count,
                      uint32_t n_lists, uint32_t n_queries, uint32_t k_in, uint32_t k,
                      uint64_t* out_idx, float* out_dist, uint32_t* out_count);
