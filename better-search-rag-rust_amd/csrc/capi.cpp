@@ -452,6 +452,17 @@ static int root_merge(bsr_comm* c, uint32_t nq, uint32_t k, uint64_t* out_idx, f
 static int root_merge_device(bsr_comm* c, bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx,
                              float* out_dist, uint32_t* out_count) {
     hipStream_t s = ix->stream;
+    if (c->host_fn) {
+        // host transport: the gathered lists arrived in c->h_* (pinned); 1 MB up at P = 8
+        const size_t nk = (size_t)nq * k * c->size;
+        BSR_TRY(c->recv_idx.ensure(nk * sizeof(uint64_t)));
+        BSR_TRY(c->recv_dist.ensure(nk * sizeof(float)));
+        BSR_TRY(c->recv_cnt.ensure((size_t)nq * c->size * sizeof(uint32_t)));
+        BSR_HIP(hipMemcpyAsync(c->recv_idx.p, c->h_idx.data(), nk * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        BSR_HIP(hipMemcpyAsync(c->recv_dist.p, c->h_dist.data(), nk * sizeof(float), hipMemcpyHostToDevice, s));
+        BSR_HIP(hipMemcpyAsync(c->recv_cnt.p, c->h_cnt.data(), (size_t)nq * c->size * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, s));
+    }
     BSR_TRY(c->nan_word.ensure(sizeof(uint32_t)));
     BSR_TRY(c->h_nan.resize(1));
     BSR_HIP(hipMemsetAsync(c->nan_word.p, 0xff, sizeof(uint32_t), s));
@@ -544,9 +555,10 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     }
     // (the root merges on the device into its own result buffer: only after its own search
     // succeeded, i.e. that buffer is sized for this batch)
-    const bool dev_merge = !c->host_fn && ok && device_merge_fits((uint32_t)c->size, k, k);
+    // (host transport: the root's lists come up to its GPU for the same merge)
+    const bool dev_merge = ok && device_merge_fits((uint32_t)c->size, k, k);
     BSR_TRY(exchange_lists(c, ok ? li : nullptr, ok ? ld : nullptr, ok ? lc : nullptr, !ok, nq, k,
-                           c->host_fn ? nullptr : ix->stream, !dev_merge));
+                           c->host_fn ? nullptr : ix->stream, !dev_merge || c->host_fn));
     if (ok) bsr_index_collect_profile_impl(ix);
     if (root && dev_merge) BSR_TRY(root_merge_device(c, ix, nq, k, out_idx, out_dist, out_count));
     else if (root) BSR_TRY(root_merge(c, nq, k, out_idx, out_dist, out_count));
