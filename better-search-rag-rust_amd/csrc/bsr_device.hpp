@@ -67,10 +67,47 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
     uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x) {
-    int lo = __shfl_up((int)(uint32_t)x, 1, kWave);
-    int hi = __shfl_up((int)(uint32_t)(x >> 32), 1, kWave);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+// Cross-lane moves inside the VALU (no LDS round trip: __shfl* lower to ds_bpermute):
+// DPP quad_perm / row rotations / row_mirror / wave_shr and v_permlane16/32_swap.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppc(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+// The value lane (lane ^ M) holds, for a constant M in {1, 2, 4, 8, 16, 32}.
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t x) {
+    if constexpr (M == 1) return dppc<0xB1>(x);        // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return dppc<0x4E>(x);   // quad_perm [2,3,0,1]
+    else if constexpr (M == 4) {
+        const uint32_t up = dppc<0x12C>(x);  // row_ror:12 -> lane + 4 (within its row of 16)
+        const uint32_t dn = dppc<0x124>(x);  // row_ror:4  -> lane - 4
+        return (lane_id() & 4) ? dn : up;
+    } else if constexpr (M == 8) return dppc<0x128>(x);  // row_ror:8 -> lane ^ 8
+    else if constexpr (M == 16) {
+        // odd rows of the first operand swap with even rows of the second: with both = x,
+        // r[1] holds row r+1 in even rows, r[0] holds row r-1 in odd rows
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane_id() & 16) ? (uint32_t)r[0] : (uint32_t)r[1];
+    } else {
+        static_assert(M == 32, "xor 1..32");
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane_id() & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+    }
+}
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t x, int m) {  // m a constant after unrolling
+    switch (m) {
+        case 1: return xor_lane32<1>(x);
+        case 2: return xor_lane32<2>(x);
+        case 4: return xor_lane32<4>(x);
+        case 8: return xor_lane32<8>(x);
+        case 16: return xor_lane32<16>(x);
+        default: return xor_lane32<32>(x);
+    }
+}
+__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x) {  // lane - 1 (lane 0: its own)
+    const uint32_t lo = dppc<0x138>((uint32_t)x);          // wave_shr:1
+    const uint32_t hi = dppc<0x138>((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
@@ -79,9 +116,16 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int m) {
-    int lo = __shfl_xor((int)(uint32_t)x, m, kWave);
-    int hi = __shfl_xor((int)(uint32_t)(x >> 32), m, kWave);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+    const uint32_t lo = xor_lane32((uint32_t)x, m);
+    const uint32_t hi = xor_lane32((uint32_t)(x >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+// The value lane 63 - lane holds: row_mirror (lane ^ 15 within its row), then ^ 16, ^ 32.
+__device__ __forceinline__ uint64_t reverse64(uint64_t x) {
+    uint32_t lo = dppc<0x140>((uint32_t)x), hi = dppc<0x140>((uint32_t)(x >> 32));
+    lo = xor_lane32<32>(xor_lane32<16>(lo));
+    hi = xor_lane32<32>(xor_lane32<16>(hi));
+    return ((uint64_t)hi << 32) | lo;
 }
 // Ascending bitonic sort of one key per lane across the wave (21 compare-exchange steps).
 __device__ __forceinline__ uint64_t wave_sort64(uint64_t x) {
@@ -149,11 +193,10 @@ struct WaveTopK {
     // (min/max against the reversed batch leaves two bitonic halves, each sorted by a
     // 6-step half-cleaner; the larger half moves on to the next register).
     __device__ __forceinline__ void merge_batch(uint64_t x) {
-        const int lane = lane_id();
         x = wave_sort64(x);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const uint64_t xr = shfl64(x, 63 - lane);
+            const uint64_t xr = reverse64(x);
             const uint64_t lo = v[e] < xr ? v[e] : xr;
             const uint64_t hi = v[e] < xr ? xr : v[e];
             v[e] = bitonic_clean64(lo);
