@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_filter(GemmArgs p) {
                             float mx = v[0];
 #pragma unroll
                             for (int r = 1; r < 16; ++r) mx = fmaxf(mx, v[r]);
-                            mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                            mx = fmaxf(mx, __uint_as_float(xor_lane32<32>(__float_as_uint(mx))));
                             if (lane < 32) srow[(rt * BM + wr * 128 + m * 32) / 32] = mx;
                         }
                         stored = true;
@@ -803,8 +803,8 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
                 float mx = v[0];
 #pragma unroll
                 for (int i = 1; i < 8; ++i) mx = fmaxf(mx, v[i]);
-                mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-                mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                mx = fmaxf(mx, __uint_as_float(xor_lane32<16>(__float_as_uint(mx))));
+                mx = fmaxf(mx, __uint_as_float(xor_lane32<32>(__float_as_uint(mx))));
                 if (h == 0) srow[g] = mx;
             }
         }
@@ -882,8 +882,8 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
                 *reinterpret_cast<float4*>(srow + u * 16 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
             } else {
                 float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-                mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-                mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                mx = fmaxf(mx, __uint_as_float(xor_lane32<16>(__float_as_uint(mx))));
+                mx = fmaxf(mx, __uint_as_float(xor_lane32<32>(__float_as_uint(mx))));
                 smax = fmaxf(smax, mx);
                 if ((u & 1) && h == 0) srow[u >> 1] = smax;  // second half of the block
                 if (u & 1) smax = -INFINITY;

@@ -130,14 +130,20 @@ __global__ void k_rows_to_bf16n(const float* __restrict__ rows, const float* __r
 // the row-side half of the certification bound.  Zero rows give q = 0 and e = 0 (the
 // reference scores them 1.0 = cosine 0, which is exactly the filter's value).
 // ------------------------------------------------------------------------------------
+// (butterflies in the VALU: the partner's value by DPP / permlane moves, bsr_device.hpp)
+__device__ __forceinline__ double xor_lane_f64(double v, int o) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = xor_lane32((uint32_t)u, o), hi = xor_lane32((uint32_t)(u >> 32), o);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    for (int o = 32; o >= 1; o >>= 1) v += xor_lane_f64(v, o);
     return v;
 }
 __device__ __forceinline__ double wave_max_f64(double v) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, xor_lane_f64(v, o));
     return v;
 }
 // Smallest f32 >= x (x >= 0, finite).
