@@ -104,6 +104,16 @@ __device__ __forceinline__ uint32_t xor_lane32(uint32_t x, int m) {  // m a cons
         default: return xor_lane32<32>(x);
     }
 }
+// Butterfly reductions over the wave (xor 32, 16, ..., 1), every lane gets the result.
+template <class F>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v, F op) {
+    v = op(v, xor_lane32<32>(v));
+    v = op(v, xor_lane32<16>(v));
+    v = op(v, xor_lane32<8>(v));
+    v = op(v, xor_lane32<4>(v));
+    v = op(v, xor_lane32<2>(v));
+    return op(v, xor_lane32<1>(v));
+}
 __device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x) {  // lane - 1 (lane 0: its own)
     const uint32_t lo = dppc<0x138>((uint32_t)x);          // wave_shr:1
     const uint32_t hi = dppc<0x138>((uint32_t)(x >> 32));

@@ -133,11 +133,8 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                         hmin = min(hmin, (uint32_t)(x[j] >> 32));
                         hmax = max(hmax, (uint32_t)(x[j] >> 32));
                     }
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    hmin = min(hmin, xor_lane32(hmin, off));
-                    hmax = max(hmax, xor_lane32(hmax, off));
-                }
+                hmin = wave_reduce_u32(hmin, [](uint32_t a, uint32_t b) { return min(a, b); });
+                hmax = wave_reduce_u32(hmax, [](uint32_t a, uint32_t b) { return max(a, b); });
                 const uint32_t diff = hmin ^ hmax;
                 const int top = diff ? 31 - __builtin_clz(diff) : -1;
                 // (top < 0: every key has the same high word)
@@ -488,8 +485,7 @@ __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint3
         // rows emitted by the filter over the batch (a statistic; one wave, no atomics)
         uint32_t sum = 0;
         for (uint32_t q = threadIdx.x; q < nq; q += kWave) sum += emit_cnt[q];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += xor_lane32(sum, off);
+        sum = wave_reduce_u32(sum, [](uint32_t a, uint32_t b) { return a + b; });
         if (threadIdx.x == 0) cur_status[kStEmitted] = sum;
     }
     if (e >= (uint64_t)nq * k) return;
