@@ -61,7 +61,8 @@ struct SeenSet {
 struct Scratch {
     std::vector<Entry> concat;
     SeenSet seen;
-    std::vector<uint32_t> pos;
+    std::vector<uint32_t> pos, cnt;
+    std::vector<float> head;
 };
 
 // One query.  Returns the output count, or UINT32_MAX on a NaN distance.
@@ -70,6 +71,8 @@ uint32_t merge_one(const ListsView& in, uint32_t q, uint32_t k, uint64_t* out_id
     const uint32_t L = in.n_lists;
     size_t total = 0;
     bool sorted = true;
+    s.cnt.resize(L);
+    s.head.resize(L);
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t c = in.count_of(l, q);
         const float* d = in.dist_of(l, q);
@@ -77,39 +80,46 @@ uint32_t merge_one(const ListsView& in, uint32_t q, uint32_t k, uint64_t* out_id
             if (d[i] != d[i]) return UINT32_MAX;  // partial_cmp().unwrap() panics
             if (i && d[i] < d[i - 1]) sorted = false;
         }
+        s.cnt[l] = c;
+        s.head[l] = c ? d[0] : __builtin_inff();
         total += c;
     }
-    s.seen.reset(std::min<size_t>(total, k));
+    // seen indices: a linear scan of the output for short lists, the hash set beyond
+    const bool small = k <= 32;
+    if (!small) s.seen.reset(std::min<size_t>(total, k));
     uint32_t out = 0;
     auto take = [&](uint64_t idx, float dist) {
-        if (!s.seen.insert(idx)) return;
+        if (small) {
+            for (uint32_t i = 0; i < out; ++i)
+                if (out_idx[i] == idx) return;
+        } else if (!s.seen.insert(idx)) {
+            return;
+        }
         out_idx[out] = idx;
         out_dist[out] = dist;
         ++out;
     };
     if (sorted) {
-        // P-way merge; ties -> lower list number, then list position (= concatenation order)
+        // P-way merge; ties -> lower list number, then list position (= concatenation order).
+        // Exhausted lists hold +inf heads and are skipped by their count.
         s.pos.assign(L, 0);
-        while (out < k) {
-            int best = -1;
+        for (size_t taken = 0; out < k && taken < total; ++taken) {
+            uint32_t best = UINT32_MAX;
             float bd = 0.0f;
-            for (uint32_t l = 0; l < L; ++l) {
-                if (s.pos[l] >= in.count_of(l, q)) continue;
-                const float d = in.dist_of(l, q)[s.pos[l]];
-                if (best < 0 || d < bd) {
-                    best = (int)l;
-                    bd = d;
+            for (uint32_t l = 0; l < L; ++l)
+                if (s.pos[l] < s.cnt[l] && (best == UINT32_MAX || s.head[l] < bd)) {
+                    best = l;
+                    bd = s.head[l];
                 }
-            }
-            if (best < 0) break;
             const uint32_t p = s.pos[best]++;
             take(in.idx_of(best, q)[p], bd);
+            if (p + 1 < s.cnt[best]) s.head[best] = in.dist_of(best, q)[p + 1];
         }
         return out;
     }
     s.concat.clear();
     for (uint32_t l = 0; l < L; ++l) {
-        const uint32_t c = in.count_of(l, q);
+        const uint32_t c = s.cnt[l];
         const uint64_t* ix = in.idx_of(l, q);
         const float* d = in.dist_of(l, q);
         for (uint32_t i = 0; i < c; ++i) s.concat.push_back({ix[i], d[i]});
@@ -128,10 +138,10 @@ int merge_top_k_lists(const ListsView& in, uint32_t n_queries, uint32_t k, uint6
                       uint32_t* out_count) {
     if (!n_queries) return BSR_OK;
     if (k == 0) return set_error(BSR_E_INVALID, "k must be >= 1");
-    // threads: ~one per 64k list entries of work, at most 8 (host cores beside the GPU)
+    // threads: one per 1M list entries of work (starting a thread costs tens of us), at most 8
     const size_t work = (size_t)n_queries * in.n_lists * std::max<uint32_t>(in.k_in, 1);
     unsigned hw = std::thread::hardware_concurrency();
-    unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)(hw ? hw : 1), work / 65536 + 1, (size_t)n_queries});
+    unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)(hw ? hw : 1), work / 1048576 + 1, (size_t)n_queries});
     std::vector<uint32_t> bad(nt, UINT32_MAX);
     auto run = [&](unsigned t) {
         Scratch s;
