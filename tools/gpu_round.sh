@@ -20,6 +20,8 @@ timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 2 --verify 2 --
 rc=$?; echo "bench c4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --config c5 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_c5.json" 2>> "$O/bench.err"
 rc=$?; echo "bench c5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --config c1 --steps 50 --warmup 5 > "$O/bench_c1.json" 2>> "$O/bench.err"
+rc=$?; echo "bench c1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --config c2 --filter bf16 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_c2_bf16.json" 2>> "$O/bench.err"
 rc=$?; echo "bench c2 bf16 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 
