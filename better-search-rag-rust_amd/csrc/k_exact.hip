@@ -522,6 +522,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
     __shared__ uint64_t s_idx[kMergeMaxEntries];
     __shared__ uint64_t s_key[kMergeMaxEntries];
     __shared__ float s_dist[kMergeMaxEntries];
+    __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
     if (q >= nq) return;
@@ -562,6 +563,37 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
         }
         return;
     }
+    // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
+    // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
+    // hash's empty mark, takes the pairwise check instead.)
+    bool has_empty_mark = false;
+    for (uint32_t j = lane; j < total; j += kWave) has_empty_mark |= s_idx[j] == ~0ull;
+    const bool pairwise = __ballot(has_empty_mark) != 0;
+    uint32_t hmask = 127;
+    while (hmask + 1 < 2 * total && hmask + 1 < kMergeMaxEntries) hmask = 2 * hmask + 1;  // load <= 1
+    auto slot0 = [&](uint64_t x) -> uint32_t {
+        uint64_t h = x * 0x9E3779B97F4A7C15ull;
+        return (uint32_t)(h >> 40) & hmask;
+    };
+    if (!pairwise) {
+        for (uint32_t i = lane; i <= hmask; i += kWave) {
+            h_idx[i] = ~0ull;
+            h_min[i] = ~0ull;
+        }
+        __syncthreads();
+        for (uint32_t j = lane; j < total; j += kWave) {
+            const uint64_t x = s_idx[j];
+            for (uint32_t sl = slot0(x);; sl = (sl + 1) & hmask) {
+                const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&h_idx[sl]), ~0ull,
+                                                (unsigned long long)x);
+                if (prev == ~0ull || prev == x) {
+                    atomicMin(reinterpret_cast<unsigned long long*>(&h_min[sl]), (unsigned long long)s_key[j]);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
     WaveTopK<E> L;
     L.init();
     uint64_t thr = kKeyNone;
@@ -571,8 +603,14 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
         if (j < total) {
             key = s_key[j];
             const uint64_t x = s_idx[j];
-            for (uint32_t i = 0; i < total; ++i)  // an earlier-sorting copy of the same index
-                if (s_idx[i] == x && s_key[i] < key) { key = kKeyNone; break; }
+            if (!pairwise) {
+                uint32_t sl = slot0(x);
+                while (h_idx[sl] != x) sl = (sl + 1) & hmask;
+                if (h_min[sl] != key) key = kKeyNone;
+            } else {
+                for (uint32_t i = 0; i < total; ++i)  // an earlier-sorting copy of the same index
+                    if (s_idx[i] == x && s_key[i] < key) { key = kKeyNone; break; }
+            }
         }
         L.offer(key, (int)k, thr);
     }
