@@ -360,6 +360,24 @@ def main():
         step()
     prof_st = index.profile(reset=True)
 
+    # The same steps without the exchange (each rank's local search alone, bsr_local_top_k):
+    # the step time's split into local search and exchange + root merge (N > 1).
+    index.set_profile(0)
+    for _ in range(2):
+        lib.bsr_local_top_k(index._h, qdev.data_ptr(), Q, K, oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st_l = lib.bsr_local_top_k(index._h, qdev.data_ptr(), Q, K, oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+        if st_l != 0:
+            raise bsr.BsrError(st_l, lib.bsr_last_error().decode())
+    local_s = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([local_s], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        local_s = float(t.item())
+    local_ms = local_s / args.steps * 1e3
+
     # p50 single-query latency over the whole corpus (configs[3] path), all ranks.
     lat = []
     index.set_profile(0)
@@ -466,6 +484,8 @@ def main():
                 " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else
                 " (exact f32 scan, HBM-bound)"),
             "roofline": roof,
+            "local_search_ms_per_step": round(local_ms, 4),
+            "exchange_ms_per_step": round(ms_per_step - local_ms, 4) if world > 1 else None,
             "kernels_ms_per_step_rank0": {  # separate profiled pass of n_stage steps (every stage evented)
                 "filter_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
                 "filter_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
