@@ -448,7 +448,8 @@ static int root_merge(bsr_comm* c, uint32_t nq, uint32_t k, uint64_t* out_idx, f
 // The root's merge on the device (RCCL path): the gathered lists in c->recv_* are merged by
 // k_merge_lists into the index's result buffer (where the local lists were), read back with
 // one D2H copy, then handed to the caller's arrays -- instead of P lists to the host and a
-// host merge (1-2 ms for 1000 queries x 8 ranks).
+// host merge (at 8 ranks x 1000 queries: a 1 MB copy and 0.15-0.3 ms of host merge, against
+// a 10 us kernel).
 static int root_merge_device(bsr_comm* c, bsr_index* ix, uint32_t nq, uint32_t k, uint64_t* out_idx,
                              float* out_dist, uint32_t* out_count) {
     hipStream_t s = ix->stream;
