@@ -134,6 +134,8 @@ def run_c1(args):
     qdev = torch.empty((Q, D), dtype=torch.float32, device=dev)
     bsr.synth_uniform(qdev.data_ptr(), 0, Q, D, 43)
     bsr.synth_uniform(qdev[0:1].data_ptr(), 0, 1, D, 42)
+    if corpus_bf16:  # the corpus holds row 0's bf16 rounding: query 0 is that row exactly
+        qdev[0:1] = qdev[0:1].to(torch.bfloat16).to(torch.float32)
     torch.cuda.synchronize()
     rows_h, q_h = corpus.cpu().numpy(), qdev.cpu().numpy()
     del corpus
@@ -290,6 +292,8 @@ def main():
     qdev = torch.empty((Q, D), dtype=torch.float32, device=dev)
     bsr.synth_uniform(qdev.data_ptr(), 0, Q, D, 43)
     bsr.synth_uniform(qdev[0:1].data_ptr(), 0, 1, D, 42)
+    if corpus_bf16:  # the corpus holds row 0's bf16 rounding: query 0 is that row exactly
+        qdev[0:1] = qdev[0:1].to(torch.bfloat16).to(torch.float32)
     torch.cuda.synchronize()
 
     comm = None
@@ -422,13 +426,17 @@ def main():
     if rank == 0:
         launches = max(prof.gemm_emit_launches, 1)
         emit_ms = prof.gemm_emit_ms / launches
-        traffic = None
+        # roofline.traffic: HBM bytes per launch from the committed PMC passes (not read in
+        # this run: rocprofv3 --pmc runs are separate, MI355X_MICROARCH.md); the source is named
+        traffic, traffic_src = None, None
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
                 for e in pm.get("entries", [pm]):
                     if e.get("rows") == n_local and e.get("queries") == Q and e.get("filter") == args.filter:
                         traffic = e.get("hbm_bytes_per_launch")
+                        traffic_src = (f"from {os.path.relpath(args.pmc_json, ROOT)} (run {e.get('run', pm.get('run', '?'))}, "
+                                       "FETCH_SIZE x 2 + WRITE_SIZE, separate rocprofv3 --pmc passes)")
             except (OSError, ValueError):
                 traffic = None
         if args.filter == "i8" and Q <= 16:
@@ -439,7 +447,8 @@ def main():
             gbs = sbytes / (emit_ms * 1e-3) / 1e9 if emit_ms > 0 else None
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1) if gbs else None,
                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4) if gbs else None,
-                    "traffic": traffic, "algorithmic_bytes_per_launch": sbytes, "avg_launch_ms": round(emit_ms, 5)}
+                    "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes_per_launch": sbytes,
+                    "avg_launch_ms": round(emit_ms, 5)}
         else:
             flops = 2.0 * Q * n_local * D
             achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
@@ -451,6 +460,7 @@ def main():
             roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2) if achieved else None,
                     "peak": peak / 1e12, "unit": "TOP/s" if args.filter == "i8" else "TFLOP/s",
                     "frac": round(achieved * 1e12 / peak, 4) if achieved else None, "traffic": traffic,
+                    "traffic_source": traffic_src,
                     "algorithmic_ops_per_launch": flops, "avg_launch_ms": round(emit_ms, 5),
                     "note": "rank 0's shard; ops = 2 * queries * shard rows * dim (int8 multiply-adds)"}
         out = {

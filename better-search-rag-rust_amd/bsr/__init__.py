@@ -27,6 +27,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -38,6 +40,7 @@ LIB_PATH = os.environ.get("BSR_LIB") or os.path.join(os.path.dirname(_PKG), "lib
 VSTORE_LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr_vstore.so")
 
 BSR_OK = 0
+BSR_PARTIAL = 1  # parallel search root: valid result without its own block (include/bsr.h)
 BSR_F32 = 0
 BSR_BF16 = 1
 BSR_MAX_K = 256
@@ -409,18 +412,22 @@ class Comm:
 
 def _as_comm(world) -> Optional[Comm]:
     """A Comm for `world`: a Comm as is, None (one rank) as None, a torch.distributed
-    group (or the default group, passed as a group object) as a cached host-transport Comm."""
+    group (or the default group, passed as a group object) as a cached host-transport Comm.
+    The cache holds the group weakly: a destroyed group's Comm is never handed to a new
+    group that reuses its id()."""
     if world is None or isinstance(world, Comm):
         return world
-    key = id(world)
-    c = _HOST_COMMS.get(key)
+    try:
+        c = _HOST_COMMS.get(world)
+    except TypeError:  # a group object that cannot be weakly referenced: no caching
+        return Comm.host(world)
     if c is None:
         c = Comm.host(world)
-        _HOST_COMMS[key] = c
+        _HOST_COMMS[world] = c
     return c
 
 
-_HOST_COMMS: dict = {}
+_HOST_COMMS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 # ---- a-2 ... a-6 (reference-shaped, single query) -------------------------------------
@@ -500,8 +507,7 @@ def gather_global_top_k(world, local_idx, local_dist, local_count, top_k: int):
     """a-4 + a-5 composed (the exchange step of parallel_top_k_similarity_search,
     src/mpi_helpers/metrics.rs:194-202) for a batch: local lists [Q, top_k] (+ counts [Q]) of
     this rank, or all None for an empty contribution.  Root: (idx, dist, count) of the
-    global top-k; other ranks: None."""
-    comm = _as_comm(world)
+    global top-k; other ranks: None.  `world` None (one rank): the local lists merged alone."""
     if local_idx is None:
         q = None
     else:
@@ -509,9 +515,22 @@ def gather_global_top_k(world, local_idx, local_dist, local_count, top_k: int):
         local_dist = np.ascontiguousarray(local_dist, np.float32)
         local_count = np.ascontiguousarray(local_count, np.uint32)
         q = local_idx.shape[0]
+        # the library reads Q * top_k entries of each list and Q counts
+        if local_idx.shape != (q, top_k) or local_dist.shape != (q, top_k) or local_count.shape != (q,):
+            raise BsrError(-1, f"local lists must be [Q, top_k] = [{q}, {top_k}] (+ counts [Q]); got "
+                               f"{local_idx.shape}, {local_dist.shape}, {local_count.shape}")
+    comm = _as_comm(world)
+    if comm is None:
+        if q is None:
+            raise BsrError(-1, "one rank (world=None) with no local lists: nothing to merge")
+        return merge_top_k_lists(local_idx[None], local_dist[None], local_count[None], top_k)
     nq = q if q is not None else 0
     # every rank must agree on the batch size: take it from the ranks that have lists
     nq = int(max(np.frombuffer(b"".join(comm.allgather_bytes(np.uint32(nq).tobytes())), np.uint32)))
+    if q is not None and q != nq:
+        # a mismatched list exchange is undefined: take part with an empty list, then fail
+        _ = lib().bsr_gather_global_top_k(comm._h, None, None, None, nq, top_k, None, None, None)
+        raise BsrError(-1, f"this rank has {q} queries, another has {nq}")
     oi = np.empty((nq, top_k), np.uint64)
     od = np.empty((nq, top_k), np.float32)
     oc = np.empty(nq, np.uint32)
@@ -522,22 +541,54 @@ def gather_global_top_k(world, local_idx, local_dist, local_count, top_k: int):
     return oi, od, oc
 
 
+def _check_parallel(status: int, rank: int) -> None:
+    """Status of bsr_parallel_top_k_similarity_search: BSR_PARTIAL on the root is the
+    reference's Some(..) after a local error (src/mpi_helpers/metrics.rs:185-202): the result
+    stands (it covers the other ranks) and the error is reported as a warning, as the
+    reference prints it."""
+    if status == BSR_PARTIAL and rank == ROOT:
+        warnings.warn(lib().bsr_last_error().decode(), RuntimeWarning, stacklevel=3)
+        return
+    _check(status)
+
+
 def parallel_top_k_similarity_search(world, rank: int, size: int, index: Index, top_k: int,
                                      target_vector) -> Optional[List[Tuple[int, float]]]:
     """src/mpi_helpers/metrics.rs:174-206, one query: the local search on this rank's shard
     (GPU), the exchange over `world` (a Comm -- RCCL or host transport --, a
     torch.distributed group, or None for one rank) and the root's merge, all inside the
     library (bsr_parallel_top_k_similarity_search).  Root: the global top-k; others: None."""
-    q = np.asarray(target_vector, np.float32).reshape(1, -1)
+    res = parallel_top_k_similarity_search_batch(world, index, np.asarray(target_vector, np.float32).reshape(1, -1),
+                                                 top_k, rank=rank)
+    if res is None:
+        return None
+    oi, od, oc = res
+    return [(int(oi[0, i]), float(od[0, i])) for i in range(int(oc[0]))]
+
+
+def parallel_top_k_similarity_search_batch(world, index: Optional[Index], queries, top_k: int,
+                                           rank: Optional[int] = None):
+    """The same for a batch of queries [Q, dim] (host array or device tensor): Q independent
+    reference searches in one collective call.  Root: (idx [Q, top_k] u64, dist [Q, top_k]
+    f32, count [Q] u32); other ranks: None.  A non-root rank whose local step fails raises
+    after the exchange; the root then warns and returns the other ranks' global top-k."""
     comm = _as_comm(world)
-    oi = np.empty((1, top_k), np.uint64)
-    od = np.empty((1, top_k), np.float32)
-    oc = np.empty(1, np.uint32)
-    _check(lib().bsr_parallel_top_k_similarity_search(comm._h if comm else None, index._h, _ptr(q), 1, top_k,
-                                                      _ptr(oi), _ptr(od), _ptr(oc)))
+    if rank is None:
+        rank = comm.rank if comm is not None else ROOT
+    if isinstance(queries, np.ndarray) or not hasattr(queries, "data_ptr"):
+        queries = np.ascontiguousarray(queries, np.float32)
+        if queries.ndim == 1:
+            queries = queries.reshape(1, -1)
+    nq = int(queries.shape[0])
+    oi = np.empty((nq, top_k), np.uint64)
+    od = np.empty((nq, top_k), np.float32)
+    oc = np.empty(nq, np.uint32)
+    st = lib().bsr_parallel_top_k_similarity_search(comm._h if comm else None, index._h if index else None,
+                                                    _ptr(queries), nq, top_k, _ptr(oi), _ptr(od), _ptr(oc))
+    _check_parallel(st, rank)
     if rank != ROOT:
         return None
-    return [(int(oi[0, i]), float(od[0, i])) for i in range(int(oc[0]))]
+    return oi, od, oc
 
 
 def calculate_accuracy_metrics(top_k_results, query_idx: int, top_k: int):

@@ -94,7 +94,14 @@ struct bsr_comm {
     std::vector<uint32_t> m_cnt;
     DevBuf nan_word;               // device merge: the lowest query with a NaN distance
     PinnedVec<uint32_t> h_nan;
+    DevBuf hdr_send, hdr_recv;     // the parallel search's shape agreement (RCCL)
+    PinnedVec<int32_t> h_hdr;      // [1 + size][kHdrWords]: this rank's words, then every rank's
 };
+
+// The parallel search's header, all-gathered before the lists: every rank's batch shape
+// and local status, so that no rank issues a list exchange the others do not match.
+constexpr size_t kHdrWords = 4;  // {n_queries, k, local status, magic}
+constexpr int32_t kHdrMagic = 0x42535231;
 
 // Copy to a caller buffer that may be host or device memory.
 #define BSR_HIP_OR_HOST_COPY(dst, src, bytes)                                            \
@@ -126,6 +133,7 @@ const char* bsr_last_error(void) { return last_error_cstr(); }
 const char* bsr_status_string(int s) {
     switch (s) {
         case BSR_OK: return "BSR_OK";
+        case BSR_PARTIAL: return "BSR_PARTIAL";
         case BSR_E_INVALID: return "BSR_E_INVALID";
         case BSR_E_NONFINITE: return "BSR_E_NONFINITE";
         case BSR_E_HIP: return "BSR_E_HIP";
@@ -253,6 +261,10 @@ static int global_top_k_impl(const uint64_t* idx, const float* dist, const uint3
         if (bad != ~0u) return set_error(BSR_E_NONFINITE, "NaN distance in query %u (the reference panics)", bad);
         return BSR_OK;
     }
+    // host counts: every array must be host memory (the host merge dereferences them all)
+    if (is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count) ||
+        (n_lists && k_in && (is_device_ptr(idx) || is_device_ptr(dist))))
+        return set_error(BSR_E_INVALID, "host counts need host lists and outputs (or pass every array on the device)");
     return merge_top_k_lists(ListsView{idx, dist, count, n_lists, n_queries, k_in}, n_queries, k, out_idx, out_dist,
                              out_count);
 }
@@ -482,9 +494,14 @@ static int gather_impl(bsr_comm* c, const uint64_t* local_idx, const float* loca
                        uint32_t nq, uint32_t k, uint64_t* root_idx, float* root_dist, uint32_t* root_count) {
     if (!c) return set_error(BSR_E_INVALID, "null communicator");
     if (!nq) return BSR_OK;
-    if (!local_idx || !local_dist || !local_count || k == 0) return set_error(BSR_E_INVALID, "bad argument");
-    if (c->rank == 0 && (!root_idx || !root_dist || !root_count)) return set_error(BSR_E_INVALID, "null root output");
-    BSR_TRY(exchange_lists(c, local_idx, local_dist, local_count, false, nq, k, c->stream));
+    if (k == 0) return set_error(BSR_E_INVALID, "k must be >= 1");
+    // bad local or root arguments: still take part (an empty contribution), then fail, so
+    // that no other rank is left blocked in the collective
+    const bool empty = !local_idx || !local_dist || !local_count;
+    const bool bad_root = c->rank == 0 && (!root_idx || !root_dist || !root_count);
+    BSR_TRY(exchange_lists(c, local_idx, local_dist, local_count, empty, nq, k, c->stream));
+    if (empty) return set_error(BSR_E_INVALID, "null local list (an empty contribution was sent)");
+    if (bad_root) return set_error(BSR_E_INVALID, "null root output");
     if (c->rank == 0) {
         const size_t nk = (size_t)nq * k * c->size;
         BSR_HIP_OR_HOST_COPY(root_idx, c->h_idx.data(), nk * sizeof(uint64_t));
@@ -506,10 +523,11 @@ static int gather_global_impl(bsr_comm* c, const uint64_t* local_idx, const floa
     if (!nq) return BSR_OK;
     if (k == 0) return set_error(BSR_E_INVALID, "k must be >= 1");
     const bool root = c->rank == 0;
-    if (root && (!out_idx || !out_dist || !out_count)) return set_error(BSR_E_INVALID, "null root output");
     const bool empty = !local_idx || !local_dist || !local_count;  // an empty contribution
     BSR_TRY(exchange_lists(c, local_idx, local_dist, local_count, empty, nq, k, c->stream));
     if (!root) return clear_counts(out_count, nq);
+    // (checked after the exchange: no other rank is left blocked in the collective)
+    if (!out_idx || !out_dist || !out_count) return set_error(BSR_E_INVALID, "null root output");
     return root_merge(c, nq, k, out_idx, out_dist, out_count);
 }
 
@@ -519,15 +537,54 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
     BSR_GUARD(gather_global_impl(comm, local_idx, local_dist, local_count, n_queries, k, out_idx, out_dist, out_count));
 }
 
+// All-gather of every rank's header {nq, k, local status, magic} into c->h_hdr[1 + r] (a
+// 16-byte collective on c->stream, or through the host transport).
+static int exchange_header(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
+    const size_t P = (size_t)c->size, hb = kHdrWords * sizeof(int32_t);
+    BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));
+    int32_t* h = c->h_hdr.data();
+    h[0] = (int32_t)nq;
+    h[1] = (int32_t)k;
+    h[2] = st;
+    h[3] = kHdrMagic;
+    if (c->host_fn) {
+        if (c->host_fn(h, h + kHdrWords, hb, c->host_user) != 0)
+            return set_error(BSR_E_RCCL, "host all-gather callback failed");
+        return BSR_OK;
+    }
+    BSR_HIP(hipSetDevice(c->device));
+    BSR_TRY(c->hdr_send.ensure(hb));
+    BSR_TRY(c->hdr_recv.ensure(hb * P));
+    BSR_HIP(hipMemcpyAsync(c->hdr_send.p, h, hb, hipMemcpyHostToDevice, c->stream));
+    BSR_NCCL(ncclAllGather(c->hdr_send.p, c->hdr_recv.p, hb, ncclUint8, c->comm, c->stream));
+    BSR_HIP(hipMemcpyAsync(h + kHdrWords, c->hdr_recv.p, hb * P, hipMemcpyDeviceToHost, c->stream));
+    BSR_HIP(stream_wait(c->stream));
+    return BSR_OK;
+}
+
+// parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206).  Collective-safe:
+// every rank reaches the same collectives whatever fails locally.
+//   1. local checks, then compute_local_top_k on this rank's shard (:185);
+//   2. (size > 1) an all-gather of every rank's header {nq, k, status}: if the ranks disagree
+//      on the batch shape, EVERY rank returns BSR_E_INVALID and no list exchange happens
+//      (mismatched all-gathers are undefined);
+//   3. gather_top_k_results (:194): a rank whose search or checks failed contributes an empty
+//      list, as the reference's error branch does (:185-191);
+//   4. the root's merge (:200-202).
+// Returns: BSR_OK; on a non-root rank whose local step failed, that error; on a root whose
+// own local step failed but whose outputs are usable, BSR_PARTIAL with the other ranks'
+// global top-k in out_* (the reference's root returns Some(..) there, :199-202).
 static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
                          uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
-    if (!ix) return set_error(BSR_E_INVALID, "null index");
     const bool root = !c || c->rank == 0;
-    if (nq && root && (!out_idx || !out_dist || !out_count)) return set_error(BSR_E_INVALID, "null output");
-    if (c && !c->host_fn && c->device != ix->device)
-        return set_error(BSR_E_INVALID, "communicator and index on different devices");
+    const bool outs_ok = !nq || (out_idx && out_dist && out_count);
+    int st = BSR_OK;
+    if (!ix) st = set_error(BSR_E_INVALID, "null index");
+    else if (root && !outs_ok) st = set_error(BSR_E_INVALID, "null output");
+    else if (c && !c->host_fn && c->device != ix->device)
+        st = set_error(BSR_E_INVALID, "communicator and index on different devices");
     // compute_local_top_k (:185-191)
-    const int st = ix->search_device(queries, nq, k);
+    if (st == BSR_OK) st = ix->search_device(queries, nq, k);
     if (!c) {  // one rank, no communicator: the local lists are the result
         BSR_TRY(st);
         if (!nq) return BSR_OK;
@@ -535,40 +592,62 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         bsr_index_collect_profile_impl(ix);
         return BSR_OK;
     }
-    if (!nq) return st;
-    if (k == 0) return st != BSR_OK ? st : set_error(BSR_E_INVALID, "k must be >= 1");
-    // A rank whose local search failed still takes part in the exchange with an empty list,
-    // as the reference does (:185-191), so no other rank blocks in the collective; it returns
-    // its own error afterwards.  The root's lists then cover the other ranks.
     std::string local_err;
     if (st != BSR_OK) local_err = last_error_cstr();
+    if (c->size > 1) {
+        BSR_TRY(exchange_header(c, nq, k, st));
+        const int32_t* h = c->h_hdr.data() + kHdrWords;
+        for (int32_t r = 0; r < c->size; ++r) {
+            const int32_t* hr = h + (size_t)r * kHdrWords;
+            if (hr[3] != kHdrMagic || hr[0] != h[0] || hr[1] != h[1])
+                return set_error(BSR_E_INVALID,
+                                 "ranks disagree on the batch shape: rank 0 (n_queries %d, k %d), rank %d "
+                                 "(n_queries %d, k %d); no rank exchanged lists",
+                                 h[0], h[1], r, hr[0], hr[1]);
+        }
+    }
+    if (!nq) return st;
+    if (k == 0) return st != BSR_OK ? st : set_error(BSR_E_INVALID, "k must be >= 1");
     const bool ok = st == BSR_OK;
     // gather_top_k_results (:194) on the index's stream (ordered after the search), then the
     // root's merge (:200-202)
     // (RCCL: the device lists; host transport: their pinned host mirror)
-    const uint64_t* li = ix->d_idx;
-    const float* ld = ix->d_dist;
-    const uint32_t* lc = ix->d_cnt;
-    if (c->host_fn) {
+    const uint64_t* li = nullptr;
+    const float* ld = nullptr;
+    const uint32_t* lc = nullptr;
+    if (ok && c->host_fn) {
         li = reinterpret_cast<const uint64_t*>(ix->h_res + ix->res_off_idx);
         ld = reinterpret_cast<const float*>(ix->h_res + ix->res_off_dist);
         lc = reinterpret_cast<const uint32_t*>(ix->h_res + ix->res_off_cnt);
+    } else if (ok) {
+        li = ix->d_idx;
+        ld = ix->d_dist;
+        lc = ix->d_cnt;
     }
     // (the root merges on the device into its own result buffer: only after its own search
-    // succeeded, i.e. that buffer is sized for this batch)
-    // (host transport: the root's lists come up to its GPU for the same merge)
+    // succeeded, i.e. that buffer is sized for this batch; host transport: the root's lists
+    // come up to its GPU for the same merge)
     const bool dev_merge = ok && device_merge_fits((uint32_t)c->size, k, k);
-    BSR_TRY(exchange_lists(c, ok ? li : nullptr, ok ? ld : nullptr, ok ? lc : nullptr, !ok, nq, k,
-                           c->host_fn ? nullptr : ix->stream, !dev_merge || c->host_fn));
+    hipStream_t xs = c->host_fn ? nullptr : (ok ? ix->stream : c->stream);
+    BSR_TRY(exchange_lists(c, li, ld, lc, !ok, nq, k, xs, !dev_merge || c->host_fn));
     if (ok) bsr_index_collect_profile_impl(ix);
-    if (root && dev_merge) BSR_TRY(root_merge_device(c, ix, nq, k, out_idx, out_dist, out_count));
-    else if (root) BSR_TRY(root_merge(c, nq, k, out_idx, out_dist, out_count));
-    else if (dev_merge) {
+    if (root && dev_merge) {
+        BSR_TRY(root_merge_device(c, ix, nq, k, out_idx, out_dist, out_count));
+    } else if (root && outs_ok) {
+        BSR_TRY(root_merge(c, nq, k, out_idx, out_dist, out_count));
+    } else if (!root && dev_merge) {
         BSR_HIP(stream_wait(ix->stream));  // the all-gather has read this rank's lists
         BSR_TRY(clear_counts(out_count, nq));
-    } else BSR_TRY(clear_counts(out_count, nq));
-    if (!ok) return set_error(st, "%s", local_err.c_str());
-    return BSR_OK;
+    } else if (!root) {
+        BSR_TRY(clear_counts(out_count, nq));
+    }
+    if (ok) return BSR_OK;
+    if (root && outs_ok) {
+        set_error(BSR_PARTIAL, "this rank's local search failed (%s); the result covers the other ranks' blocks",
+                  local_err.c_str());
+        return BSR_PARTIAL;
+    }
+    return set_error(st, "%s", local_err.c_str());
 }
 
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries, uint32_t n_queries,

@@ -58,30 +58,48 @@ __global__ void k_widen_bf16_rows(const uint16_t* __restrict__ src, uint64_t n, 
 
 // ------------------------------------------------------------------------------------
 // Row magnitudes exactly as src/metrics.rs:154: sqrt of the sequential f32 sum of a_i*a_i.
-// One lane per row; the per-row dependency chain is inherently serial.
+// One lane per row (the per-row dependency chain is inherently serial), but the rows reach
+// the lanes through LDS: each wave owns 64 consecutive rows and stages them 64 columns at a
+// time with coalesced 16-byte loads (16 lanes per 256-byte row segment), then every lane
+// walks its own row's staged segment in index order.  (Round 2's lane-per-row float4 loads
+// touched 64 rows per wave-instruction and fetched 3.6x the slab.)  Requires ld % 64 == 0
+// (rows zero-padded to ld, kLdAlign).
 // ------------------------------------------------------------------------------------
-__global__ void k_row_norms(const float* __restrict__ rows, uint64_t n, uint32_t dim,
-                            uint32_t ld, float* __restrict__ na, uint32_t* flags) {
-    const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint32_t f = 0;
-    if (r < n) {
-        const float* a = rows + r * ld;
-        float acc = -0.0f;
-        bool bad = false;
-        uint32_t i = 0;
-        for (; i + 4 <= dim; i += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(a + i);
-            bad = bad || !isfinite(x.x) || !isfinite(x.y) || !isfinite(x.z) || !isfinite(x.w);
-            acc = acc + x.x * x.x;
-            acc = acc + x.y * x.y;
-            acc = acc + x.z * x.z;
-            acc = acc + x.w * x.w;
+__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ rows, uint64_t n, uint32_t dim,
+                                                   uint32_t ld, float* __restrict__ na, uint32_t* flags) {
+    constexpr int kCols = 64, kPitch = kCols + 1;  // odd pitch: lane l reads bank (l + j) % 32
+    __shared__ float tile[4][64 * kPitch];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+    float* t = tile[w];
+    float acc = -0.0f;
+    bool bad = false;
+    for (uint32_t c0 = 0; c0 < dim; c0 += kCols) {
+        const uint32_t cw = dim - c0 < (uint32_t)kCols ? dim - c0 : (uint32_t)kCols;
+        const uint32_t col = (lane & 15) * 4;
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t rr = i * 4 + (lane >> 4);
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (r0 + rr < n) v = *reinterpret_cast<const float4*>(rows + (r0 + rr) * ld + c0 + col);
+            float* d = t + rr * kPitch + col;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
         }
-        for (; i < dim; ++i) {
-            const float x = a[i];
+        __syncthreads();
+        const float* a = t + lane * kPitch;
+        for (uint32_t j = 0; j < cw; ++j) {
+            const float x = a[j];
             bad |= !isfinite(x);
             acc = acc + x * x;
         }
+        __syncthreads();
+    }
+    const uint64_t r = r0 + lane;
+    uint32_t f = 0;
+    if (r < n) {
         const float m = __builtin_sqrtf(acc);
         na[r] = m;
         if (bad) f |= kRowNonFinite;

@@ -168,10 +168,6 @@ hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint6
                              uint64_t* part, hipStream_t s);
 hipError_t launch_merge_parts(const uint64_t* part, uint32_t grid, const int32_t* qids,
                               uint32_t nqf, uint32_t k, uint64_t* out_keys, hipStream_t s);
-// Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
-// result buffer the next search will use.
-// status: the NEXT search's status words (zeroed); emit_cnt (optional): per-query emitted
-// counts, summed into cur_status[kStEmitted].
 // The root's merge of gathered [P][nq][k_in] lists (counts [P][nq]) into [nq][k] outputs on
 // the device (compute_global_top_k); P <= 64, P * k_in <= kMergeMaxEntries, k <= 256.
 // *first_nan must hold ~0 before the launch; afterwards the lowest query with a NaN distance.
@@ -179,6 +175,10 @@ constexpr uint32_t kMergeMaxEntries = 1024;
 hipError_t launch_merge_lists(const uint64_t* idx, const float* dist, const uint32_t* cnt, uint32_t P, uint32_t nq,
                               uint32_t k_in, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count,
                               uint32_t* first_nan, hipStream_t s);
+// Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
+// result buffer the next search will use.
+// status: the NEXT search's status words (zeroed); emit_cnt (optional): per-query emitted
+// counts, summed into cur_status[kStEmitted].
 hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64_t n,
                            uint64_t offset, uint64_t* out_idx, float* out_dist,
                            uint32_t* out_count, uint32_t* status, const uint32_t* emit_cnt,

@@ -3,8 +3,8 @@
  * block-distributed exact cosine-distance scan + global top-k reduction.
  *
  * One process per GPU (the reference's one process per MPI rank).  Every entry point
- * returns 0 (BSR_OK) or a negative bsr_status; bsr_last_error() gives a thread-local
- * message.  No C++ exception or panic crosses this boundary.  Plain pointers only: query,
+ * returns 0 (BSR_OK) or a negative bsr_status (BSR_PARTIAL, positive, only from the
+ * parallel search's root: see there); bsr_last_error() gives a thread-local message.  No C++ exception or panic crosses this boundary.  Plain pointers only: query,
  * row and output pointers may be host or device (hipMalloc) memory, detected per call.
  *
  * Each entry point names the reference item it replaces (paths relative to the reference
@@ -43,6 +43,7 @@ extern "C" {
 #endif
 
 typedef enum {
+    BSR_PARTIAL = 1,      /* parallel search root: result valid but its own block is missing */
     BSR_OK = 0,
     BSR_E_INVALID = -1,   /* bad argument / null pointer / k out of range */
     BSR_E_NONFINITE = -2, /* NaN or Inf in a query or row (the reference panics) */
@@ -185,11 +186,15 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
                             uint64_t* out_idx, float* out_dist, uint32_t* out_count);
 
 /* ---- a-6: parallel_top_k_similarity_search: local search on this rank's shard,
- * RCCL all-gather of the partial lists (bsr_gather_global_top_k), host merge.  Root gets
- * the global top-k in out_*; other ranks get out_count[q] = 0 (the reference's None).
- * comm may be NULL for a single-rank run (no exchange).  A rank whose local search fails
- * still completes the exchange with an empty list (:185-191) and then returns its error;
- * the root's lists cover the other ranks. --------------------------------------------- */
+ * RCCL all-gather of the partial lists (bsr_gather_global_top_k), root merge (on the
+ * root's GPU).  Root gets the global top-k in out_*; other ranks get out_count[q] = 0 (the
+ * reference's None).  comm may be NULL for a single-rank run (no exchange).
+ * Collective-safe: with size > 1 the ranks first all-gather {n_queries, k, local status}
+ * (16 bytes); if they disagree on n_queries or k, every rank returns BSR_E_INVALID and no
+ * lists are exchanged.  A rank whose local step fails (bad arguments, device mismatch, a
+ * failed search) still completes the exchange with an empty list (:185-191): a non-root
+ * rank then returns its error; the root returns BSR_PARTIAL with the other ranks' global
+ * top-k in out_* (the reference's root still returns Some(..), :199-202). ------------- */
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries,
                                          uint32_t n_queries, uint32_t k, uint64_t* out_idx,
                                          float* out_dist, uint32_t* out_count);

@@ -167,3 +167,51 @@ def test_gloo_exchange_edge_cases(tmp_path, oracle_mod):
     wi, wd, wc = oracle_mod.parallel_top_k(rows, qs, 6, size=1)
     assert np.array_equal(r["oc"], wc) and np.array_equal(r["oi"], wi)
     assert np.array_equal(r["od"].view(np.uint32), wd.view(np.uint32))
+
+
+def _worker_collective_safety(rank, world, port, out_path):
+    """bsr_parallel_top_k_similarity_search's collective safety without a GPU: every rank
+    passes no index (a local failure before any search), so the library's own header
+    exchange, empty contributions and root merge run over gloo.  Then one rank passes a
+    different batch size: every rank must be rejected, none left blocked."""
+    import warnings
+    dist = _init(rank, world, port)
+    import bsr
+
+    comm = bsr.Comm.host(dist.group.WORLD)
+    q = np.zeros((4, D), np.float32)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        try:
+            res = bsr.parallel_top_k_similarity_search_batch(comm, None, q, K)
+            st = 0
+        except bsr.BsrError as e:
+            res, st = None, e.status
+        warned = "|".join(str(x.message) for x in w)
+    try:
+        bsr.parallel_top_k_similarity_search_batch(comm, None, q[:3] if rank == world - 1 else q, K)
+        st2, msg2 = 0, ""
+    except bsr.BsrError as e:
+        st2, msg2 = e.status, str(e)
+    dist.barrier()
+    np.savez(f"{out_path}.{rank}.npz", st=st, st2=st2, msg2=np.frombuffer((msg2 or " ").encode(), np.uint8),
+             warned=np.frombuffer((warned or " ").encode(), np.uint8),
+             cnt=res[2] if res is not None else np.zeros(0, np.uint32), none=res is None)
+    comm.close()
+    dist.destroy_process_group()
+
+
+def test_gloo_parallel_search_collective_safety(tmp_path):
+    world = 3
+    out = str(tmp_path / "cs")
+    mp.spawn(_worker_collective_safety, args=(world, _free_port(), out), nprocs=world, join=True)
+    r = [np.load(f"{out}.{i}.npz") for i in range(world)]
+    # no index anywhere: the root reports BSR_PARTIAL (a warning) with every list empty;
+    # the other ranks raise their local error
+    assert int(r[0]["st"]) == 0 and not bool(r[0]["none"]) and not r[0]["cnt"].any() and len(r[0]["cnt"]) == 4
+    assert b"null index" in r[0]["warned"].tobytes()
+    for i in range(1, world):
+        assert int(r[i]["st"]) == -1 and bool(r[i]["none"])
+    # batch sizes that disagree: all ranks rejected, collectively
+    for i in range(world):
+        assert int(r[i]["st2"]) == -1 and b"disagree on the batch shape" in r[i]["msg2"].tobytes()

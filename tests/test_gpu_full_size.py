@@ -9,9 +9,9 @@ generator the index was loaded from) and merged as the reference merges rank blo
 
 Sizes: configs[1] 1M x 1000 (top-10); configs[2] 10M as the 8 interval_by_rank shards of
 8 GPUs, loaded one at a time with their global offsets, and as one 10M shard; configs[3]
-10M x single queries (the skinny path, graph replay); configs[4] the 6.25M-row bf16 shard
-of 50M over 8 GPUs x 4096 queries, top-100 (4.8 GB of int8 filter rows: row offsets past
-4 GiB)."""
+10M x single queries (the skinny path, graph replay); configs[4] 50M bf16 rows as the 8
+interval_by_rank shards of 8 GPUs (6.25M rows, 4.8 GB of int8 filter rows each: row offsets
+past 4 GiB) x 4096 queries, top-100, merged on the device as the RCCL root merges."""
 import os
 
 import numpy as np
@@ -193,26 +193,54 @@ def test_configs3_10m_single_queries(bsr_mod, oracle_mod, index_10m):
     assert want[0][0, 0] == 0 and want[0][3, 0] == n - 2
 
 
-# ---- configs[4]: 6.25M bf16 rows (one of 8 shards of 50M) x 4096, top-100 --------------------
-def test_configs4_bf16_shard_x_4096_top100(bsr_mod, oracle_mod, gpu):
-    n, nq, k = 6_250_000, 4096, 100
-    rows = _gen(bsr_mod, n, bf16=True)
-    ix = bsr_mod.Index(D, max_k=k, device=0, dtype=bsr_mod.BSR_BF16)
-    ix.load(rows, 0)
-    del rows
-    _torch().cuda.empty_cache()
+# ---- configs[4]: 50M bf16 rows as 8 shards of 6.25M x 4096 queries, top-100 ------------------
+def test_configs4_bf16_50m_8_shards_x_4096_top100(bsr_mod, oracle_mod, gpu):
+    """configs[4]: the 8 interval_by_rank(r, 8, 50M) bf16 shards (6.25M rows each, 4.8 GB of
+    int8 filter rows: row offsets past 4 GiB) searched one at a time with their global offsets
+    (up to 43.75M), x 4096 queries, k = 100, then merged by k_merge_lists -- the RCCL root's
+    device merge -- and checked against the host merge.  Properties on every query of every
+    shard and of the merge; 4 queries bit for bit vs the oracle over all 50M rows (one planted
+    in shard 7, one at a shard boundary)."""
     torch = _torch()
+    n, nq, k, P = 50_000_000, 4096, 100, 8
+    plant = [(0, 0), (1, n - 1), (2, 43_750_123), (3, 6_250_000), (4, 31_000_007)]
     q = _gen(bsr_mod, nq, 0, seed=43)
-    for pos, row in ((0, 0), (1, n - 1), (2, 6_000_000)):   # rows past 4 GiB of int8 operand
+    for pos, row in plant:   # the bf16-rounded corpus rows themselves
         q[pos] = _gen(bsr_mod, 1, row, bf16=True).to(torch.float32)[0]
     torch.cuda.synchronize()
-    got = _search_device(ix, q, k)
-    st = ix.last_stats()
-    assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
-    _check_properties(got, n, k, "configs[4]")
-    for pos, row in ((0, 0), (1, n - 1), (2, 6_000_000)):
-        assert got[0][pos, 0] == row and got[1][pos, 0] == 0.0
-    sub = [0, 1, 2, 3, 2048, 4095]
+    li = torch.empty((P, nq, k), dtype=torch.int64, device="cuda:0")
+    ld = torch.empty((P, nq, k), dtype=torch.float32, device="cuda:0")
+    lc = torch.empty((P, nq), dtype=torch.int32, device="cuda:0")
+    for r in range(P):
+        iv = bsr_mod.interval_by_rank(r, P, n)
+        s, cnt = iv.start_index, iv.get_count()
+        rows = _gen(bsr_mod, cnt, s, bf16=True)
+        ix = bsr_mod.Index(D, max_k=k, device=0, dtype=bsr_mod.BSR_BF16)
+        ix.load(rows, s)
+        del rows
+        torch.cuda.empty_cache()
+        ix.local_top_k_device(q, nq, k, li[r], ld[r], lc[r])
+        st = ix.last_stats()
+        assert st.n_fallback == 0 and st.n_exact_direct == 0, (r, st.n_fallback, st.n_exact_direct)
+        got_r = (li[r].cpu().numpy().astype(np.uint64), ld[r].cpu().numpy(), lc[r].cpu().numpy().astype(np.uint32))
+        assert (got_r[2] == k).all() and ((got_r[0] >= s) & (got_r[0] < s + cnt)).all(), r
+        _check_properties((got_r[0] - np.uint64(s), got_r[1], got_r[2]), cnt, k, f"configs[4] shard {r}")
+        ix.close()
+        torch.cuda.empty_cache()
+    # the root's device merge (k_merge_lists: P = 8 lists of k_in = 100 per query)
+    oi = torch.empty((nq, k), dtype=torch.int64, device="cuda:0")
+    od = torch.empty((nq, k), dtype=torch.float32, device="cuda:0")
+    oc = torch.empty(nq, dtype=torch.int32, device="cuda:0")
+    st = bsr_mod.lib().bsr_global_top_k(li.data_ptr(), ld.data_ptr(), lc.data_ptr(), P, nq, k, k, oi.data_ptr(),
+                                        od.data_ptr(), oc.data_ptr())
+    assert st == 0, bsr_mod.lib().bsr_last_error()
+    got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
+    _check_properties(got, n, k, "configs[4] merged")
+    host = bsr_mod.merge_top_k_lists(li.cpu().numpy().astype(np.uint64), ld.cpu().numpy(),
+                                     lc.cpu().numpy().astype(np.uint32), k)
+    assert all(np.array_equal(a, b) for a, b in zip(got, host)), "device merge != host merge"
+    for pos, row in plant:
+        assert got[0][pos, 0] == row and got[1][pos, 0] == 0.0, (pos, row, got[0][pos, :3])
+    sub = [0, 2, 3, 4095]
     want = _chunked_oracle(bsr_mod, oracle_mod, n, q[sub].cpu().numpy(), k, bf16=True)
     _assert_same(got, want, sub, "configs[4] vs oracle")
-    ix.close()

@@ -114,3 +114,24 @@ def test_device_merge_rejects_mixed_memory(bsr_mod):
     st = bsr_mod.lib().bsr_global_top_k(li.data_ptr(), ld.data_ptr(), lc.data_ptr(), 1, 1, 2, 2,
                                         oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
     assert st != 0
+
+
+def test_host_merge_rejects_device_lists(bsr_mod):
+    """Host counts with device lists or outputs: rejected (BSR_E_INVALID), never
+    dereferenced on the CPU."""
+    import torch
+    li = torch.zeros((1, 1, 2), dtype=torch.int64, device="cuda")
+    ld = torch.zeros((1, 1, 2), dtype=torch.float32, device="cuda")
+    lc = np.full((1, 1), 2, np.uint32)
+    oi = np.empty((1, 2), np.uint64)
+    od = np.empty((1, 2), np.float32)
+    oc = np.empty(1, np.uint32)
+    st = bsr_mod.lib().bsr_global_top_k(li.data_ptr(), ld.data_ptr(), lc.ctypes.data, 1, 1, 2, 2,
+                                        oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+    assert st == -1
+    hi = np.zeros((1, 1, 2), np.uint64)
+    hd = np.zeros((1, 1, 2), np.float32)
+    doi = torch.empty((1, 2), dtype=torch.int64, device="cuda")
+    st = bsr_mod.lib().bsr_global_top_k(hi.ctypes.data, hd.ctypes.data, lc.ctypes.data, 1, 1, 2, 2,
+                                        doi.data_ptr(), od.ctypes.data, oc.ctypes.data)
+    assert st == -1

@@ -394,6 +394,51 @@ def test_small_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu):
     assert dev_replays > 0
 
 
+@pytest.mark.parametrize("staging", ["device", "host"])
+def test_large_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu, staging):
+    """Filtered batches of Q >= 256 replay a captured graph (prep -> sample pass -> tau0 ->
+    emit filter -> rescore -> finalize -> D2H) from their second search of a shape on.  Same
+    buffer (device pointer, or the library's host staging copy), same shape, new contents every
+    round -- one round turns some queries into corpus rows, another into a scaled row -- and
+    every round must equal the oracle on ALL queries (a stale tau0, candidate count or query
+    operand baked into the graph would show here).  Each call is an independent search
+    (src/mpi_helpers/metrics.rs:174-206)."""
+    import torch
+    rng = np.random.default_rng(77)
+    n, nq, k = 50000, 256, 10
+    rows = rng.uniform(-1, 1, (n, 768)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=16)
+    dq = torch.empty((nq, 768), dtype=torch.float32, device="cuda:0")
+    oi = torch.empty((nq, k), dtype=torch.int64, device="cuda:0")
+    od = torch.empty((nq, k), dtype=torch.float32, device="cuda:0")
+    oc = torch.empty(nq, dtype=torch.int32, device="cuda:0")
+    hq = np.empty((nq, 768), np.float32)  # one host buffer, rewritten in place
+    replays = []
+    for it in range(7):
+        qs = rng.uniform(-1, 1, (nq, 768)).astype(np.float32)
+        if it == 3:   # queries that are corpus rows (self-match at distance 0)
+            for j in range(0, nq, 17):
+                qs[j] = rows[(j * 7919 + it) % n]
+        if it == 5:   # a scaled corpus row: distance 0 without being identical
+            qs[1] = rows[123] * np.float32(4.0)
+        if staging == "device":
+            dq.copy_(torch.from_numpy(qs))
+            torch.cuda.synchronize()
+            ix.local_top_k_device(dq, nq, k, oi, od, oc)
+            got = (oi.cpu().numpy().astype(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32))
+        else:
+            hq[:] = qs
+            got = ix.local_top_k(hq, k)
+        st = ix.last_stats()
+        replays.append(st.graph_replay)
+        assert st.n_exact_direct == 0
+        _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k, size=8, threads=8), f"{staging} round {it}")
+        if it == 3:
+            for j in range(0, nq, 17):
+                assert got[0][j, 0] == (j * 7919 + it) % n and got[1][j, 0] == 0.0
+    assert replays[0] == 0 and all(replays[1:]), replays
+
+
 def test_profile_levels(bsr_mod, oracle_mod, gpu):
     """bsr_index_set_profile: level 1 times only the filter kernels (events bound to their
     dispatch), 2 every stage, 0 none -- results identical at every level."""
