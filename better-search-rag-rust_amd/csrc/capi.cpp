@@ -300,7 +300,7 @@ static int comm_init_impl(const uint8_t id[BSR_UNIQUE_ID_BYTES], int32_t rank, i
         delete c;
         return set_error(BSR_E_RCCL, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {  // blocking: see bsr_index
         ncclCommDestroy(c->comm);
         delete c;
         return set_error(BSR_E_HIP, "hipStreamCreate failed");

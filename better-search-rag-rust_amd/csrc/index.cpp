@@ -254,7 +254,12 @@ int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
     ix->ld = (uint32_t)round_up(cfg->dim, kLdAlign);
     ix->op = (cfg->flags & BSR_FLAG_FILTER_BF16) ? kFilterBF16 : kFilterI8;
     ix->op_row_bytes = ix->op == kFilterBF16 ? ix->ld * 2 : ix->ld;
-    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
+    // A blocking stream: its work waits for work issued earlier on the legacy default (NULL)
+    // stream -- PyTorch's default stream -- so device rows or queries a caller has just
+    // produced there are complete before the library reads them (the ABI has no stream
+    // argument).  Round 3's 50M test loaded shards whose bf16 conversion was still running on
+    // torch's stream into a non-blocking stream: stale rows, wrong results.
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamDefault) != hipSuccess) {
         delete ix;
         return set_error(BSR_E_HIP, "hipStreamCreate failed");
     }

@@ -4,8 +4,12 @@
  *
  * One process per GPU (the reference's one process per MPI rank).  Every entry point
  * returns 0 (BSR_OK) or a negative bsr_status (BSR_PARTIAL, positive, only from the
- * parallel search's root: see there); bsr_last_error() gives a thread-local message.  No C++ exception or panic crosses this boundary.  Plain pointers only: query,
- * row and output pointers may be host or device (hipMalloc) memory, detected per call.
+ * parallel search's root: see there); bsr_last_error() gives a thread-local message.  No
+ * C++ exception or panic crosses this boundary.  Plain pointers only: query, row and
+ * output pointers may be host or device (hipMalloc) memory, detected per call.
+ * Device inputs: the library's streams are blocking streams, so its work waits for work
+ * issued before the call on the legacy default (NULL) stream (e.g. PyTorch's default
+ * stream); data produced on any other stream must be complete (synchronized) first.
  *
  * Each entry point names the reference item it replaces (paths relative to the reference
  * repository nichmorgan/better-search-rag-rust):
