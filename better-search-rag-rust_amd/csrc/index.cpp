@@ -122,7 +122,8 @@ using namespace bsr;
 // profiling helpers
 // ---------------------------------------------------------------------------------------
 // Events exist when the index was created with BSR_FLAG_PROFILE; prof_level (bsr_index_set_profile)
-// picks which stages record them: 1 = the filter / scan kernels only, 2 = every stage.
+// picks which stages record them: 1 = the emit filter / scan kernels only (the bench's timed
+// steps: each recorded event is one more node in the search graph), 2 = every stage.
 static inline bool profiling(const bsr_index* ix) { return (ix->cfg.flags & BSR_FLAG_PROFILE) != 0; }
 static inline void ev_begin(bsr_index* ix, Events& e, int level = 2) {
     if (profiling(ix) && ix->prof_level >= level && e.a) { (void)hipEventRecord(e.a, ix->stream); e.armed = true; }
@@ -132,17 +133,17 @@ static inline void ev_end(bsr_index* ix, Events& e) {
 }
 // Events of one filter / scan kernel: handed to its launch (hipExtLaunchKernel records them at
 // the kernel's own dispatch and completion), so they time the kernel, not the stream gaps.
-static inline void ev_kernel(bsr_index* ix, Events& e, hipEvent_t& a, hipEvent_t& b) {
+static inline void ev_kernel(bsr_index* ix, Events& e, hipEvent_t& a, hipEvent_t& b, int level) {
     a = b = nullptr;
-    if (profiling(ix) && ix->prof_level >= 1 && e.a) { a = e.a; b = e.b; e.armed = true; }
+    if (profiling(ix) && ix->prof_level >= level && e.a) { a = e.a; b = e.b; e.armed = true; }
 }
 // A filter / scan kernel launch timed at profile level >= 1: inside a graph capture the events
 // are recorded on the stream around the launch (event-record nodes: the kernel plus its
 // dispatch gap), otherwise bound to the kernel's own dispatch (hipExtLaunchKernel).
 template <class F>
-static inline hipError_t launch_timed(bsr_index* ix, Events& e, F&& launch) {
+static inline hipError_t launch_timed(bsr_index* ix, Events& e, F&& launch, int level = 1) {
     if (ix->capturing) {
-        const bool timed = profiling(ix) && ix->prof_level >= 1 && e.a;
+        const bool timed = profiling(ix) && ix->prof_level >= level && e.a;
         if (timed) {
             hipError_t r = hipEventRecord(e.a, ix->stream);
             if (r != hipSuccess) return r;
@@ -156,7 +157,7 @@ static inline hipError_t launch_timed(bsr_index* ix, Events& e, F&& launch) {
         return hipSuccess;
     }
     hipEvent_t e0, e1;
-    ev_kernel(ix, e, e0, e1);
+    ev_kernel(ix, e, e0, e1, level);
     return launch(e0, e1);
 }
 static inline void ev_collect(Events& e, double& ms, uint64_t& n, uint64_t launches) {
@@ -439,7 +440,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
         BSR_HIP(launch_timed(ix, ix->ev_sample, [&](hipEvent_t e0, hipEvent_t e1) {
             return skinny ? launch_filter_skinny_sample(g, ix->stream, e0, e1)
                           : launch_filter_sample(ix->op, g, ix->stream, e0, e1);
-        }));
+        }, 2));
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
                                   ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
     } else {
@@ -632,7 +633,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         if (timed_level >= 1) {  // the captured event-record nodes ran
             ev_emit.armed = true;
-            ev_sample.armed = gs.sampled;
+            ev_sample.armed = gs.sampled && timed_level >= 2;
         }
         stats.n_candidates = kp_for(k);
         ++graph_replays;

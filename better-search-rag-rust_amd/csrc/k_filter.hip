@@ -525,25 +525,39 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     // source chunk is XOR-swizzled so that LDS chunk position p holds global chunk p ^ swz.
     const uint32_t lrow = w * 16 + (lane >> 2);
     const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
-    uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
-    uint32_t iss_ti = 0, iss_kt = 0;
-    __amdgpu_buffer_rsrc_t rsrc_a;
-    auto set_issue_tile = [&]() {
-        const uint32_t rt = g0 + iss_ti * RG;
-        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
-                                                   BM * (uint32_t)p.a_stride, 0x00020000);
-        if (!EMIT) {
-            const uint32_t r = rt * BM + lrow < p.n_rows ? lrow : p.n_rows - 1 - rt * BM;
-            aoff_dma = r * (uint32_t)p.a_stride + lchunk;
-        }
+    // Tile ti's descriptor (base = its first row) and this lane's byte offset in it (SAMPLE:
+    // tail rows read the last valid row).
+    auto tile_src = [&](uint32_t ti, __amdgpu_buffer_rsrc_t& rs, uint32_t& off) {
+        const uint32_t rt = g0 + ti * RG;
+        rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
+                                               BM * (uint32_t)p.a_stride, 0x00020000);
+        const uint32_t r = (EMIT || rt * BM + lrow < p.n_rows) ? lrow : p.n_rows - 1 - rt * BM;
+        off = r * (uint32_t)p.a_stride + lchunk;
     };
+    // Static schedule (NK > A, every dim of the product): the DMA issued during slice kt of
+    // tile t fills slice (kt + A) % NK of tile t (kt + A < NK) or of tile t + 1 -- both
+    // descriptors computed once per tile, so a DMA is two instructions and no branch.  Past
+    // the last tile the stream re-reads it (steady counted waits; nobody reads those slots).
+    constexpr bool kStatic = NK > A;
+    __amdgpu_buffer_rsrc_t rs_cur, rs_nxt;
+    uint32_t off_cur = 0, off_nxt = 0;
+    auto dma_static = [&](uint32_t jj, int kt) {
+        uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
+        if (kt + A < NK)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, off_cur, (kt + A) * kSliceB, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_nxt, (lds_void_t*)la, 16, off_nxt, (kt + A - NK) * kSliceB, 0, 0);
+    };
+    // dynamic schedule (NK <= A: a DMA may run more than one tile ahead)
+    uint32_t iss_ti = 0, iss_kt = 0, aoff_dma = 0;
+    __amdgpu_buffer_rsrc_t rsrc_a;
     auto issue_dma = [&](uint32_t jj) {
         uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma, iss_kt * kSliceB, 0, 0);
         if (++iss_kt == NK) {
             iss_kt = 0;
             ++iss_ti;
-            if (iss_ti < my_rt) set_issue_tile();
+            if (iss_ti < my_rt) tile_src(iss_ti, rsrc_a, aoff_dma);
         }
     };
     // A fragment of row block rb (rows 16rb .. +15): lane -> row 16rb + (lane & 15), chunk
@@ -557,9 +571,21 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     };
 
     i32x4v_t acc[8][2];
-    if (my_rt) set_issue_tile();
     const uint32_t pre = J ? (uint32_t)A : 0u;
-    for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
+    if (my_rt) {
+        tile_src(0, rsrc_a, aoff_dma);
+        rs_cur = rsrc_a;
+        off_cur = aoff_dma;
+        tile_src(my_rt > 1 ? 1 : 0, rs_nxt, off_nxt);
+    }
+    if (kStatic) {
+        for (uint32_t jj = 0; jj < pre; ++jj) {
+            uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, off_cur, jj * kSliceB, 0, 0);
+        }
+    } else {
+        for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
+    }
     qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
     if (J)
 #pragma unroll
@@ -567,6 +593,11 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
+        if (kStatic && t) {
+            rs_cur = rs_nxt;
+            off_cur = off_nxt;
+            tile_src(t + 1 < my_rt ? t + 1 : t, rs_nxt, off_nxt);
+        }
         float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
         // SAMPLE: one scale for the tile's 128 sampled rows (a scalar load: counted in lgkmcnt,
@@ -593,12 +624,16 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
                 // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
                 // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
-                if (bar_slice ? rb == 6 : rb == 1) issue_dma(jj + A);
+                if (bar_slice ? rb == 6 : rb == 1) {
+                    if (kStatic) dma_static(jj + A, kt);
+                    else issue_dma(jj + A);
+                }
                 // barrier (odd slices, after group 5): slices <= jj + 3 landed everywhere (the
                 // reads before the next barrier reach rows 0-1 of slice jj + 3); in flight: the
                 // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
-                // the tile's scale load
-                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
+                // the tile's scale load.  (Static schedule: also at the last slice -- the
+                // trailing DMAs keep the count steady -- so no branch.)
+                if (bar_slice && rb == 5 && (kStatic || jj + 1 < J)) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -713,211 +748,6 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     }
 }
 
-
-// ------------------------------------------------------------------------------------
-// Query-stationary int8 emit filter, one wave per SIMD: k_filter_qs64.
-//
-// k_filter_qs16 runs two waves per SIMD with 32 queries each, so every A fragment read from
-// LDS feeds two MFMAs and each 16-row block of a slice is read by all 8 waves of the CU
-// (64 KiB of ds_read_b128 per 8 KiB slice).  Here one 256-thread workgroup per CU holds the
-// same 256-query tile in FOUR waves of 64 queries: the wave's B fragments for all of K take
-// 4 x 12 x 4 = 192 registers and its accumulators 8 x 4 x 4 = 128 (the 512-entry register
-// file of a one-wave-per-SIMD kernel), every A fragment feeds FOUR MFMAs and the CU reads
-// each slice from LDS four times instead of eight: half the LDS read bytes and half the
-// fragment-read instructions per MFMA, and four waves at each barrier instead of eight.
-// Ring, swizzle, LDS-DMA stream, barriers and the two-level emission are k_filter_qs16's;
-// each wave fills 32 rows of every slice (two 1 KiB LDS-DMA instructions).
-// ------------------------------------------------------------------------------------
-template <int NK>
-__global__ __launch_bounds__(256, 1) void k_filter_qs64(GemmArgs p) {
-    constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
-    constexpr int BM = 128, BN = kFilterTile, NT = 256, SLOT = BM * kSliceB;
-    constexpr int NB = 4;                // 16-query blocks per wave
-    constexpr int CAP = 10;              // candidate ring entries per (lane, query block)
-    static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
-    static_assert(BN == 4 * NB * 16, "four waves of NB query blocks cover the query tile");
-    constexpr int EM_BYTES = NT * NB * CAP * 8;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
-    uint32_t ecnt[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) ecnt[nb] = 0;
-
-    const uint32_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const uint32_t G = (gridDim.x >> 3) / p.n_qt;
-    const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
-    const bool active = slot < G * p.n_qt;
-    const uint32_t qt = active ? slot % p.n_qt : 0;
-    const uint32_t g0 = xcd * G + (active ? slot / p.n_qt : 0);
-    const uint32_t RG = 8 * G;
-    const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
-    const uint32_t J = my_rt * NK;
-
-    // B fragments of the wave's four 16-query blocks, all K: fb[nb][kt] = query
-    // qt*256 + 64w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
-    uint32_t qq[NB];
-    i32x4v_t fb[NB][NK];
-    float tau[NB], sbq[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-        qq[nb] = qt * BN + w * 64 + nb * 16 + (lane & 15);
-        const uint8_t* src = p.B + (uint64_t)qq[nb] * p.row_bytes + 16 * (lane >> 4);
-#pragma unroll
-        for (int kt = 0; kt < NK; ++kt) fb[nb][kt] = *reinterpret_cast<const i32x4v_t*>(src + 64 * kt);
-        tau[nb] = p.tau[qq[nb]];
-        sbq[nb] = p.b_scale[qq[nb]];
-    }
-    // The B fragments live in the AGPR half of the register file (MFMA A/B operands may be
-    // AGPRs; the library builds this kernel with -amdgpu-mfma-vgpr-form, so accumulators and
-    // A fragments take the arch VGPRs): 192 + ~250 registers, no copies, no spills.
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-        for (int kt = 0; kt < NK; ++kt) asm volatile("" : "+a"(fb[nb][kt]));
-    auto flush_ring = [&](int nb) {
-        const uint32_t nn = ecnt[nb];
-        if (nn) {
-            const uint32_t gp = atomicAdd(p.cnt + qq[nb], nn);
-            for (uint32_t i = 0; i < nn; ++i)
-                if (gp + i < p.cap) p.cand[(uint64_t)qq[nb] * p.cap + gp + i] = lkeys[(nb * CAP + i) * NT];
-        }
-        ecnt[nb] = 0;
-    };
-
-    // LDS-DMA: wave w fills rows 32w .. 32w+31 of each slice, two 1 KiB instructions (rows
-    // 32w + 16i + lane/4); the source chunk XOR-swizzled as in k_filter_qs16.
-    uint32_t aoff_dma[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const uint32_t lrow = w * 32 + i * 16 + (lane >> 2);
-        aoff_dma[i] = lrow * (uint32_t)p.a_stride + ((lane & 3) ^ qs16_swz(lrow)) * 16;
-    }
-    uint32_t iss_ti = 0, iss_kt = 0;
-    __amdgpu_buffer_rsrc_t rsrc_a;
-    auto set_issue_tile = [&]() {
-        const uint32_t rt = g0 + iss_ti * RG;
-        rsrc_a = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
-                                                   BM * (uint32_t)p.a_stride, 0x00020000);
-    };
-    auto issue_dma = [&](uint32_t jj, int i) {
-        uint8_t* la = lds + (jj % S) * SLOT + (wu * 2 + i) * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)la, 16, aoff_dma[i], iss_kt * kSliceB, 0, 0);
-        if (i == 1 && ++iss_kt == NK) {
-            iss_kt = 0;
-            ++iss_ti;
-            if (iss_ti < my_rt) set_issue_tile();
-        }
-    };
-    const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
-    i32x4v_t fa[4];
-    auto read_frag = [&](uint32_t jj, int rb) {
-        fa[rb & 3] = *reinterpret_cast<const i32x4v_t*>(lds + (jj % S) * SLOT + rb * 1024 + aoff0);
-    };
-
-    i32x4v_t acc[8][NB];
-    if (my_rt) set_issue_tile();
-    const uint32_t pre = J ? (uint32_t)A : 0u;
-    for (uint32_t jj = 0; jj < pre; ++jj) {
-        issue_dma(jj, 0);
-        issue_dma(jj, 1);
-    }
-    qs_barrier(pre >= 3 ? 2 * (pre - 3) : 0);  // slices 0, 1, 2 landed everywhere
-    if (J)
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
-
-    for (uint32_t t = 0; t < my_rt; ++t) {
-        const uint32_t rt = g0 + t * RG;
-        const float4 scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
-#pragma unroll
-        for (int kt = 0; kt < NK; ++kt) {
-            const uint32_t jj = t * NK + kt;
-            const bool bar_slice = (kt & 1) == 1;
-#pragma unroll
-            for (int rb = 0; rb < 8; ++rb) {
-#pragma unroll
-                for (int nb = 0; nb < NB; ++nb) {
-                    if (kt == 0) {
-                        const i32x4v_t z = {};
-                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], z, 0, 0, 0);
-                    } else {
-                        acc[rb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[rb & 3], fb[nb][kt], acc[rb][nb], 0, 0, 0);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (rb < 4) read_frag(jj, rb + 4);
-                else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
-                // DMAs of slice jj + A: groups 1, 3 on even slices; after the barrier (groups 6,
-                // 7) on odd slices (the slot they refill, slice jj - 2's, is then free everywhere)
-                if (bar_slice ? rb == 6 : rb == 1) issue_dma(jj + A, 0);
-                if (bar_slice ? rb == 7 : rb == 3) issue_dma(jj + A, 1);
-                // barrier (odd slices, after group 5): slices <= jj + 3 landed everywhere; in
-                // flight: the DMAs of slices jj + 4, jj + 5 (2 each) and, while younger than
-                // slice jj + 3's (kt <= 2), the tile's scale load
-                if (bar_slice && rb == 5 && jj + 1 < J) qs_wait_n(4 + (kt <= 2 ? 1 : 0));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
-        const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
-        bool stored = false;
-        // level 1, one ballot per tile: the lane's integer maximum over its 32 values of each
-        // query block, scored with the tile's largest (or, for a negative maximum, smallest)
-        // block scale -- never below any of its values' scores
-        const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
-        const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
-        bool any = false;
-        int mrb[NB];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-            int m = acc[0][nb][0];
-#pragma unroll
-            for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m;
-            mrb[nb] = m;
-            any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
-        }
-        if (__ballot(any)) {
-            // level 2: per (query block, 16-row block) its maximum against tau, then the
-            // passing blocks' 4 rows appended without branches
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) {
-                if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
-                bool pass_rb[8];
-#pragma unroll
-                for (int rb = 0; rb < 8; ++rb) {
-                    const i32x4v_t& x = acc[rb][nb];
-                    const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
-                    pass_rb[rb] = ((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb];
-                }
-#pragma unroll
-                for (int rb = 0; rb < 8; ++rb) {
-                    if (!__ballot(pass_rb[rb])) continue;
-                    if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
-                        flush_ring(nb);
-                        stored = true;
-                    }
-                    const i32x4v_t& x = acc[rb][nb];
-                    const float scr = sc[rb >> 1];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float v = ((float)x[r] * scr) * sbq[nb];
-                        const uint32_t row = rt * BM + rb * 16 + 4 * (lane >> 4) + r;
-                        lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
-                        ecnt[nb] += (v >= tau[nb] && row < p.n_rows) ? 1u : 0u;
-                    }
-                }
-            }
-        }
-        if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
-    }
-    wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) flush_ring(nb);
-}
 
 // ------------------------------------------------------------------------------------
 // Skinny int8 filter for batches of at most 16 queries (single-query latency path): the
@@ -1287,27 +1117,11 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 }
 
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the query-stationary
-// kernel; other int8 widths and the bf16 operand: k_filter.  The emit pass runs k_filter_qs64
-// when kEmitQs64 is set (measured against k_filter_qs16: tools/microbench/qs64_ab.hip).
-#ifndef BSR_EMIT_QS64
-#define BSR_EMIT_QS64 0
-#endif
-constexpr bool kEmitQs64 = BSR_EMIT_QS64 != 0;
+// kernel; other int8 widths and the bf16 operand: k_filter.  (A one-wave-per-SIMD variant
+// with 64 queries per wave, tools/microbench/k_qs64_lab.hip, measured slower: DESIGN.md §5.)
 template <bool EMIT>
 static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
-    if (kEmitQs64 && EMIT && op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
-        // the emit pass: one wave per SIMD, 64 queries per wave
-        const dim3 g(grid), b(256);
-        switch (nk) {
-            case 2: BSR_KLAUNCH((k_filter_qs64<2>), g, b, s, e0, e1, a); return;
-            case 4: BSR_KLAUNCH((k_filter_qs64<4>), g, b, s, e0, e1, a); return;
-            case 6: BSR_KLAUNCH((k_filter_qs64<6>), g, b, s, e0, e1, a); return;
-            case 8: BSR_KLAUNCH((k_filter_qs64<8>), g, b, s, e0, e1, a); return;
-            case 10: BSR_KLAUNCH((k_filter_qs64<10>), g, b, s, e0, e1, a); return;
-            default: BSR_KLAUNCH((k_filter_qs64<12>), g, b, s, e0, e1, a); return;
-        }
-    }
     if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
         const dim3 g(grid), b(512);
         switch (nk) {

@@ -211,6 +211,27 @@ def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu, fflags)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "clusters")
 
 
+@pytest.mark.parametrize("k", [10, 50])
+def test_filter_outlier_block_scales(bsr_mod, oracle_mod, gpu, k):
+    """Rows with one dominant component get large int8 block scales: the emit filter's integer
+    pre-test threshold (from the LARGEST block scale of the shard) is then far below most
+    blocks' own -- a loose pre-test, but the emitted set must still be exactly the float test's
+    and every result exact.  Some queries are outlier rows themselves."""
+    rng = np.random.default_rng(8)
+    n = 60000
+    rows = rng.uniform(-1, 1, (n, 768)).astype(np.float32)
+    spikes = rng.choice(n, 300, replace=False)
+    rows[spikes, rng.integers(0, 768, 300)] = np.float32(60.0)   # max|a_i|/|a| ~ 0.96
+    qs = rng.uniform(-1, 1, (40, 768)).astype(np.float32)
+    qs[:5] = rows[spikes[:5]]
+    qs[5:10, 7] += np.float32(30.0)                              # queries leaning on one dim
+    ix = _index(bsr_mod, rows, max_k=64)
+    got = ix.local_top_k(qs, k)
+    _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k, size=8, threads=8), f"outlier scales k={k}")
+    for j in range(5):
+        assert got[0][j, 0] == spikes[j] and got[1][j, 0] == 0.0
+
+
 def test_global_offset_and_get_many(bsr_mod, gpu):
     rng = np.random.default_rng(1)
     rows = rng.uniform(-1, 1, (300, 768)).astype(np.float32)
@@ -440,8 +461,8 @@ def test_large_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu, 
 
 
 def test_profile_levels(bsr_mod, oracle_mod, gpu):
-    """bsr_index_set_profile: level 1 times only the filter kernels (events bound to their
-    dispatch), 2 every stage, 0 none -- results identical at every level."""
+    """bsr_index_set_profile: level 1 times only the emit filter / scan kernels (events bound to
+    their dispatch), 2 every stage, 0 none -- results identical at every level."""
     rng = np.random.default_rng(31)
     rows = rng.uniform(-1, 1, (30000, 768)).astype(np.float32)
     qs = rng.uniform(-1, 1, (40, 768)).astype(np.float32)
@@ -457,7 +478,8 @@ def test_profile_levels(bsr_mod, oracle_mod, gpu):
     assert seen[2].gemm_emit_launches == 1 and seen[2].select_launches == 0 and seen[2].searches == 1
     assert seen[2].rescore_launches == 1
     assert seen[1].gemm_emit_launches == 1 and seen[1].select_launches == 0 and seen[1].searches == 0
-    assert seen[1].gemm_emit_ms > 0.0
+    assert seen[1].gemm_emit_ms > 0.0 and seen[1].gemm_sample_launches == 0
+    assert seen[2].gemm_sample_launches == 1
     assert seen[0].gemm_emit_launches == 0 and seen[0].searches == 0
     with pytest.raises(bsr_mod.BsrError):
         ix.set_profile(3)

@@ -11,10 +11,17 @@
 //   kNoBar       no s_barrier (vmcnt waits only: reads may race the DMA; timing only)
 //   kNoDma       no LDS-DMA (the ring holds whatever it held: timing only)
 //   kNoLdsRead   no fragment reads (the MFMAs reuse the fragments in registers: timing only)
+//   kSameTile    every row tile's DMA reads the workgroup's FIRST tile (always L2-resident: the
+//                upside of perfect L2 sharing among the workgroups of a row-tile stream)
 namespace bsrlab {
 using namespace bsr;
 
-enum : int { kStaticDma = 1, kNoEpi = 2, kNoBar = 4, kNoDma = 8, kNoLdsRead = 16 };
+enum : int { kStaticDma = 1, kNoEpi = 2, kNoBar = 4, kNoDma = 8, kNoLdsRead = 16, kSameTile = 32 };
+// PACE > 0: the n_qt workgroups that stream the same row tiles (same g0) keep within PACE
+// tiles of each other: after each tile wave 0 publishes its count (relaxed agent-scope store,
+// progress words in p.S, zeroed before the launch); before each tile it reads the group's
+// words through the scalar path (glc) and sleeps while it leads the slowest by more than
+// PACE.  Bounded spin: stale words only slow it down.  Lab only (n_qt <= 4).
 
 template <int N>
 __device__ __forceinline__ void wait_vm_only() {
@@ -25,7 +32,7 @@ __device__ __forceinline__ void qs_wait_n_nobar(int n) {
     else wait_vm_only<2>();
 }
 
-template <int FLAGS>
+template <int FLAGS, int PACE = 0>
 __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     constexpr int NK = 12;
     constexpr bool EMIT = true;
@@ -75,7 +82,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
     const uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
     auto rsrc_for = [&](uint32_t ti) {
-        const uint32_t rt = g0 + ti * RG;
+        const uint32_t rt = g0 + ((FLAGS & kSameTile) ? 0 : ti) * RG;
         return __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
                                                  BM * (uint32_t)p.a_stride, 0x00020000);
     };
@@ -130,8 +137,20 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) fa[rb] = *reinterpret_cast<const i32x4v_t*>(lds + rb * 1024 + aoff0);
 
+    uint32_t* const prog = reinterpret_cast<uint32_t*>(p.S) + g0 * 4;
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
+        if (PACE > 0 && w == 0 && t > (uint32_t)PACE && active) {
+            typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+            for (int spin = 0; spin < 20000; ++spin) {
+                u32x4_t v;
+                asm volatile("s_load_dwordx4 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(prog) : "memory");
+                uint32_t mn = v[0];
+                for (uint32_t i = 1; i < p.n_qt; ++i) mn = min(mn, (uint32_t)v[i]);
+                if (t <= mn + (uint32_t)PACE) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
         if (FLAGS & kStaticDma) {
             if (t) {
                 rs_cur = rs_nxt;
@@ -228,6 +247,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
             }
         }
         if (stored) wait_vm0();
+        if (PACE > 0 && tid == 0) __hip_atomic_store(prog + qt, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     wait_vm0();
     if (!(FLAGS & kNoEpi)) {

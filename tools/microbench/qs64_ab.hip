@@ -1,12 +1,14 @@
-// Microbenchmark + cross-check (tooling): the emit filter k_filter_qs16<true,12> (two waves
-// per SIMD, 32 queries per wave) against k_filter_qs64<12> (one wave per SIMD, 64 queries per
-// wave) on a synthetic int8 shard, interleaved in one process (same clocks) after a settle.
-// Both must emit the same candidate set per query (sorted keys equal).
+// Microbenchmark + cross-check (tooling): the product emit filter k_filter_qs16<true,12> (two
+// waves per SIMD, 32 queries per wave) against lab variants -- k_filter_qs64<12> (one wave per
+// SIMD, 64 queries per wave, k_qs64_lab.hip) and the ablation copies of k_qs16x_lab.hip -- on
+// a synthetic int8 shard, interleaved in one process (same clocks) after a settle.  The
+// emitting variants must emit the same candidate set per query (sorted keys equal).
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../../include
-//        -I../../better-search-rag-rust_amd/csrc qs64_ab.hip -o qs64_ab
+//        -I../../better-search-rag-rust_amd/csrc -mllvm -amdgpu-mfma-vgpr-form qs64_ab.hip -o qs64_ab
 // Run:   ./qs64_ab [rows] [queries] [rounds] [tau]
 #include "k_filter.hip"
 #include "k_qs16x_lab.hip"
+#include "k_qs64_lab.hip"
 
 #include <stdio.h>
 #include <string.h>
@@ -49,6 +51,8 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&tau, qpad * 4));
     CHECK(hipMalloc(&cand, (size_t)qpad * cap * 8));
     CHECK(hipMalloc(&cnt, qpad * 4));
+    uint32_t* prog;  // pacing progress words (lab), zeroed before every launch
+    CHECK(hipMalloc(&prog, 4096 * 4));
     hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
     hipLaunchKernelGGL(fill_i8, dim3(1024), dim3(256), 0, 0, (int8_t*)B8, (size_t)qpad * ld, 4);
     hipLaunchKernelGGL(fill_f32, dim3(256), dim3(256), 0, 0, as, (size_t)npad / 32, 1.0f / (127.0f * 16.0f));
@@ -57,6 +61,7 @@ int main(int argc, char** argv) {
     bsr::GemmArgs g{};
     g.A = A8; g.B = B8; g.row_bytes = ld; g.a_stride = ld;
     g.n_rows = n; g.a_scale_rows = 32; g.n_qt = qpad / 256; g.n_rt = (n + 255) / 256;
+    g.S = reinterpret_cast<float*>(prog);
     g.a_scale = as; g.b_scale = bs; g.tau = tau; g.cand = cand; g.cnt = cnt; g.cap = cap;
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
@@ -65,10 +70,14 @@ int main(int argc, char** argv) {
     using namespace bsrlab;
     std::vector<V> vs = {
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, 512, {}},
-        {"qs64 (1 wave/SIMD)", bsr::k_filter_qs64<12>, 256, {}},
+        {"qs64 (1 wave/SIMD, lab)", bsrlab::k_filter_qs64<12>, 256, {}},
         {"qs16x static-dma", k_qs16x<kStaticDma>, 512, {}},
         {"qs16x copy", k_qs16x<0>, 512, {}},
+        {"sdma pace 2", k_qs16x<kStaticDma, 2>, 512, {}},
+        {"sdma pace 4", k_qs16x<kStaticDma, 4>, 512, {}},
+        {"sdma pace 8", k_qs16x<kStaticDma, 8>, 512, {}},
     };
+    const size_t n_main = vs.size();
     // timing-only ablations (outputs not compared)
     std::vector<V> abl = {
         {"x no-epi", k_qs16x<kNoEpi>, 512, {}},
@@ -78,6 +87,7 @@ int main(int argc, char** argv) {
         {"x no-epi no-ldsrd", k_qs16x<kNoEpi | kNoLdsRead>, 512, {}},
         {"x no-epi no-dma/rd", k_qs16x<kNoEpi | kNoDma | kNoLdsRead>, 512, {}},
         {"x no-epi/dma/rd/bar", k_qs16x<kNoEpi | kNoDma | kNoLdsRead | kNoBar>, 512, {}},
+        {"x sdma same-tile", k_qs16x<kStaticDma | kSameTile>, 512, {}},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
@@ -86,6 +96,7 @@ int main(int argc, char** argv) {
         std::vector<float> ht(qpad, tv);
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
         CHECK(hipMemset(cnt, 0, qpad * 4));
+        CHECK(hipMemset(prog, 0, 4096 * 4));
         CHECK(hipEventRecord(e0));
         hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, g);
         CHECK(hipEventRecord(e1));
@@ -121,7 +132,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 100; ++i) run(vs[i % vs.size()], tau_emit);
     for (float tv : {1e9f, tau_emit}) {
         for (auto& v : vs) v.t.clear();
-        if (tv != 1e9f) vs.resize(4);  // the ablations at tau = inf only
+        if (tv != 1e9f) vs.resize(n_main);  // the ablations at tau = inf only
         for (int r = 0; r < rounds; ++r)
             for (auto& v : vs) v.t.push_back(run(v, tv));
         for (auto& v : vs) {
