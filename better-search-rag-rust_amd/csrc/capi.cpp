@@ -537,9 +537,11 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
     BSR_GUARD(gather_global_impl(comm, local_idx, local_dist, local_count, n_queries, k, out_idx, out_dist, out_count));
 }
 
-// All-gather of every rank's header {nq, k, local status, magic} into c->h_hdr[1 + r] (a
-// 16-byte collective on c->stream, or through the host transport).
-static int exchange_header(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
+// All-gather of every rank's header {nq, k, status of the local checks, magic} into
+// c->h_hdr[1 + r]: through the host transport (synchronous), or as a 16-byte RCCL all-gather
+// on c->stream that header_wait() completes -- enqueued before the local search, so its
+// latency hides behind the search.
+static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
     const size_t P = (size_t)c->size, hb = kHdrWords * sizeof(int32_t);
     BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));
     int32_t* h = c->h_hdr.data();
@@ -558,16 +560,19 @@ static int exchange_header(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
     BSR_HIP(hipMemcpyAsync(c->hdr_send.p, h, hb, hipMemcpyHostToDevice, c->stream));
     BSR_NCCL(ncclAllGather(c->hdr_send.p, c->hdr_recv.p, hb, ncclUint8, c->comm, c->stream));
     BSR_HIP(hipMemcpyAsync(h + kHdrWords, c->hdr_recv.p, hb * P, hipMemcpyDeviceToHost, c->stream));
-    BSR_HIP(stream_wait(c->stream));
+    return BSR_OK;
+}
+static int header_wait(bsr_comm* c) {
+    if (!c->host_fn) BSR_HIP(stream_wait(c->stream));
     return BSR_OK;
 }
 
 // parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206).  Collective-safe:
 // every rank reaches the same collectives whatever fails locally.
-//   1. local checks, then compute_local_top_k on this rank's shard (:185);
-//   2. (size > 1) an all-gather of every rank's header {nq, k, status}: if the ranks disagree
-//      on the batch shape, EVERY rank returns BSR_E_INVALID and no list exchange happens
-//      (mismatched all-gathers are undefined);
+//   1. local checks; (size > 1) the all-gather of every rank's header {nq, k, status} is
+//      enqueued; then compute_local_top_k on this rank's shard (:185);
+//   2. (size > 1) the headers: if the ranks disagree on the batch shape, EVERY rank returns
+//      BSR_E_INVALID and no list exchange happens (mismatched all-gathers are undefined);
 //   3. gather_top_k_results (:194): a rank whose search or checks failed contributes an empty
 //      list, as the reference's error branch does (:185-191);
 //   4. the root's merge (:200-202).
@@ -583,8 +588,24 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     else if (root && !outs_ok) st = set_error(BSR_E_INVALID, "null output");
     else if (c && !c->host_fn && c->device != ix->device)
         st = set_error(BSR_E_INVALID, "communicator and index on different devices");
+    // the shape agreement's all-gather, issued right after the local search's GPU work is
+    // enqueued (its latency hides behind the search; issued first, its RCCL kernel would hold
+    // CUs the persistent filter needs); the header carries the local checks' status
+    const bool multi = c && c->size > 1;
+    struct HookCtx { bsr_comm* c; uint32_t nq, k; int32_t st; } hc{c, nq, k, st};
+    auto hook = [](void* p) -> int {
+        const HookCtx* h = static_cast<const HookCtx*>(p);
+        return header_start(h->c, h->nq, h->k, h->st);
+    };
+    bool header_issued = false;
     // compute_local_top_k (:185-191)
-    if (st == BSR_OK) st = ix->search_device(queries, nq, k);
+    if (st == BSR_OK) {
+        st = ix->search_device(queries, nq, k, multi ? +hook : nullptr, &hc);
+        header_issued = multi && ix->launched_hook;
+        // (a failed header all-gather is a transport error: every rank sees it; report it)
+        if (header_issued && st == BSR_E_RCCL) return st;
+    }
+    if (multi && !header_issued) BSR_TRY(header_start(c, nq, k, st));
     if (!c) {  // one rank, no communicator: the local lists are the result
         BSR_TRY(st);
         if (!nq) return BSR_OK;
@@ -594,8 +615,8 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     }
     std::string local_err;
     if (st != BSR_OK) local_err = last_error_cstr();
-    if (c->size > 1) {
-        BSR_TRY(exchange_header(c, nq, k, st));
+    if (multi) {
+        BSR_TRY(header_wait(c));
         const int32_t* h = c->h_hdr.data() + kHdrWords;
         for (int32_t r = 0; r < c->size; ++r) {
             const int32_t* hr = h + (size_t)r * kHdrWords;

@@ -386,7 +386,7 @@ static uint32_t cap_for(uint32_t k) { return 16u * (kp_for(k) + 1u); }
 
 // Candidate stage (steps 2-5) for every query of the batch.  Batches of at most 16
 // queries on an int8 index use the skinny (HBM-bound, no LDS) filter kernels.
-static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
+static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint32_t* next_status) {
     const bool skinny = ix->op == kFilterI8 && nq <= kSkinnyMaxQ;
     // k' candidates, (k'+1) % 64 == 0, about 3k: the k-th exact score must clear the (k'+1)-th
     // approximate one by E_q, and in a Gaussian-like tail that takes ~3x as many rows at
@@ -489,6 +489,12 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     ra.out_keys = ix->keys.as<uint64_t>();
     ra.fail_cnt = status + kStFail;
     ra.fail_list = ix->fail.as<uint32_t>();
+    // the result rows are written by the rescore kernels themselves (no k_finalize launch)
+    ra.res_idx = ix->d_idx;
+    ra.res_dist = ix->d_dist;
+    ra.res_cnt = ix->d_cnt;
+    ra.offset = ix->global_offset;
+    ra.n_rows = n;
     if (fused_select) {
         ra.sel = 1;
         ra.cand_keys = ix->cand.as<uint64_t>();
@@ -515,13 +521,19 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     rb.tau0 = ix->tau.as<float>();
     rb.fail_cnt = status + kStFail2;
     rb.fail_list = ix->fail2.as<uint32_t>();
+    rb.next_status = next_status;
+    rb.emit_cnt = ix->cnt.as<uint32_t>();
+    rb.cur_status = status;
+    rb.n_queries = nq;
     BSR_HIP(launch_rescore(rb, ix->stream));
     ev_end(ix, ix->ev_rescore);
     return BSR_OK;
 }
 
-int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
+int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*),
+                             void* ctx) {
     bsr_index* ix = this;
+    launched_hook = false;
     if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
     if (k == 0 || k > ix->cfg.max_k) return set_error(BSR_E_INVALID, "k=%u outside [1, max_k=%u]", k, ix->cfg.max_k);
     BSR_HIP(hipSetDevice(ix->device));
@@ -612,10 +624,12 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
             stats.n_exact_direct = nq;
             BSR_TRY(run_exact_scan(ix, qids_id.as<int32_t>(), nq, k));
         } else {
-            BSR_TRY(run_filter(ix, nq, qpad, k));
+            // (the rescore kernels write the result rows and the status bookkeeping)
+            BSR_TRY(run_filter(ix, nq, qpad, k, next_status));
         }
-        BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
-                                (use_filter && n > 0) ? cnt.as<uint32_t>() : nullptr, d_status, stream));
+        if (!(use_filter && n > 0))
+            BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,
+                                    nullptr, d_status, stream));
         ev_end(ix, ev_total);
         BSR_HIP(hipMemcpyAsync(h_res, res[cur].p, res_bytes, hipMemcpyDeviceToHost, stream));
         return BSR_OK;
@@ -666,7 +680,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k) {
         if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, false};
     }
     next_status_clean = true;
+    int hook_st = BSR_OK;
+    if (after_launch) {
+        launched_hook = true;
+        hook_st = after_launch(ctx);
+    }
     BSR_HIP(stream_wait(stream));
+    if (hook_st != BSR_OK) return hook_st;
     // Later rounds (second-chance rescore, scan) finalize and read back again, directly.
     auto finalize_and_read = [&]() -> int {
         BSR_HIP(launch_finalize(keys.as<uint64_t>(), nq, k, n, global_offset, d_idx, d_dist, d_cnt, next_status,

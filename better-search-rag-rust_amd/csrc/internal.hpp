@@ -125,6 +125,10 @@ struct bsr_index {
     ~bsr_index();
 
     // Run the local search; results stay in d_idx / d_dist / d_cnt (device, [nq][k]) and in
-    // the pinned host mirror h_res at the same offsets.
-    int search_device(const float* queries, uint32_t nq, uint32_t k);
+    // the pinned host mirror h_res at the same offsets.  after_launch (optional) runs once the
+    // search's GPU work is enqueued, before the host waits for it (the parallel search issues
+    // its shape-agreement collective there); its non-OK status is returned after the wait.
+    int search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*) = nullptr,
+                      void* ctx = nullptr);
+    bool launched_hook = false;  // after_launch ran during the last search_device
 };

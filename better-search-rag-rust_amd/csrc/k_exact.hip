@@ -91,6 +91,14 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     float* const lds = lds_all + w * STAGE;
     float* const ldq_all = lds_all + W * STAGE;
     const uint32_t n_items = a.n_items_dev ? *a.n_items_dev : a.n_items;
+    if (W > 1 && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
+        // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
+        if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
+        uint32_t sum = 0;
+        for (uint32_t q = threadIdx.x; q < a.n_queries; q += kWave) sum += a.emit_cnt[q];
+        sum = wave_reduce_u32(sum, [](uint32_t x, uint32_t y) { return x + y; });
+        if (threadIdx.x == 0) a.cur_status[kStEmitted] = sum;
+    }
     for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
         const uint32_t q = a.qlist ? a.qlist[item] : item;
         // the query, once per item (its loads are not behind the candidate prefetch); rows
@@ -284,6 +292,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         }
         if (w == 0) {
             L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
+            bool certified = false;
             if (lane == 0) {
                 // Certification: every row outside the candidate set has
                 // approximate cosine <= tau_x, hence reference cosine <= tau_x + E_q and
@@ -307,6 +316,23 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                     const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
                     a.fail_list[pos] = q;
                 }
+                certified = ok;
+            }
+            // fused finalize: certified lists (modes S / A) and every second-chance item (mode
+            // B) become result rows now; the first pass's uncertified ones are left to mode B
+            if (a.res_idx && (W > 1 || __shfl((int)certified, 0, kWave))) {
+                const uint32_t cnt = (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const uint32_t i = e * kWave + lane;
+                    if (i < a.k) {
+                        const uint64_t key = L.v[e];
+                        const bool has = i < cnt && key != kKeyNone;
+                        a.res_idx[(uint64_t)q * a.k + i] = has ? a.offset + key_row(key) : ~0ull;
+                        a.res_dist[(uint64_t)q * a.k + i] = has ? key_dist(key) : INFINITY;
+                    }
+                }
+                if (lane == 0) a.res_cnt[q] = cnt;
             }
         }
     }

@@ -154,6 +154,19 @@ struct RescoreArgs {
     uint64_t* out_keys;         // [nq][k]
     uint32_t* fail_cnt;         // uncertified queries: count (a status word) and list
     uint32_t* fail_list;
+    // Fused finalize (the filter path: no k_finalize launch): the list of a query becomes its
+    // (global index, distance) result rows here -- modes S / A for the certified queries, mode
+    // B for every item it rescored (the uncertified ones are rewritten after the exact scan).
+    uint64_t* res_idx;          // [nq][k] (nullptr: no fused finalize)
+    float* res_dist;
+    uint32_t* res_cnt;          // [nq]
+    uint64_t offset, n_rows;    // global index of local row 0; shard rows (count = min(k, n))
+    // mode B: block 0 also zeroes the NEXT search's status words and sums the emitted counts
+    // into cur_status[kStEmitted] (what k_finalize does on the other paths)
+    uint32_t* next_status;
+    const uint32_t* emit_cnt;
+    uint32_t* cur_status;
+    uint32_t n_queries;
 };
 // Workgroups of the device-counted rescore (failed certifications, usually a few queries).
 constexpr uint32_t kRescoreAllGrid = 128;
