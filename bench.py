@@ -436,7 +436,7 @@ def main():
                 for e in pm.get("entries", [pm]):
                     if e.get("rows") == n_local and e.get("queries") == Q and e.get("filter") == args.filter:
                         traffic = e.get("hbm_bytes_per_launch")
-                        traffic_src = (f"from {os.path.relpath(args.pmc_json, ROOT)} (run {e.get('run', pm.get('run', '?'))}, "
+                        traffic_src = (f"from {os.path.relpath(args.pmc_json, ROOT)} (run {e.get('run') or pm.get('run', '?')}, "
                                        "FETCH_SIZE x 2 + WRITE_SIZE, separate rocprofv3 --pmc passes)")
             except (OSError, ValueError):
                 traffic = None

@@ -2,10 +2,11 @@
 
 usage: python tools/diag/timeline.py <kernel_trace.csv> [min_searches]
 
-A search is the kernel sequence k_query_prep ... k_finalize on one queue.  Prints, over the
-searches after the first few (steady state): the average duration of each kernel, the span
-prep-start -> finalize-end, the kernels' busy time inside it, the idle gaps between them,
-and the turnaround finalize-end -> next prep-start (host wait, readback, Python, launch)."""
+A search is the kernel sequence from one k_query_prep to the last kernel before the next one
+(k_finalize or, since round 3, the second-chance k_rescore that finalizes in place).  Prints,
+over the searches after the first few (steady state): the average duration of each kernel,
+the span first-start -> last-end, the kernels' busy time inside it, the idle gaps between
+them, and the turnaround last-end -> next prep-start (host wait, readback, Python, launch)."""
 import collections
 import csv
 import statistics
@@ -27,7 +28,16 @@ def main():
             searches.append(cur)
         elif cur is not None:
             cur.append((s, e, name))
-    searches = [sr for sr in searches if any("k_finalize" in n for _, _, n in sr)]
+    # (a search's kernels follow each other within 1 ms; later launches belong to other work)
+    trimmed = []
+    for sr in searches:
+        body = [sr[0]]
+        for x in sr[1:]:
+            if x[0] - body[-1][1] > 1_000_000:
+                break
+            body.append(x)
+        trimmed.append(body)
+    searches = trimmed
     steady = searches[skip:]
     if not steady:
         print("no complete searches")
@@ -35,8 +45,7 @@ def main():
     dur = collections.defaultdict(list)
     spans, busys, turns = [], [], []
     for i, sr in enumerate(steady):
-        fin = max(j for j, (_, _, n) in enumerate(sr) if "k_finalize" in n)
-        body = sr[:fin + 1]
+        body = sr
         for s, e, n in body:
             dur[n.split("(")[0]].append((e - s) / 1e3)
         spans.append((body[-1][1] - body[0][0]) / 1e3)
@@ -47,7 +56,7 @@ def main():
     print(f"searches: {len(steady)} (after {skip})")
     for n, v in sorted(dur.items(), key=lambda kv: -statistics.mean(kv[1]) * len(kv[1])):
         print(f"  {statistics.mean(v):9.2f} us  x{len(v) / len(steady):4.2f}/search  {n}")
-    print(f"span prep->finalize  {statistics.median(spans):9.2f} us (median)")
+    print(f"span first->last     {statistics.median(spans):9.2f} us (median)")
     print(f"kernels busy         {statistics.median(busys):9.2f} us")
     print(f"gaps between kernels {statistics.median(spans) - statistics.median(busys):9.2f} us")
     if turns:

@@ -32,11 +32,12 @@ __device__ __forceinline__ void qs_wait_n_nobar(int n) {
     else wait_vm_only<2>();
 }
 
-template <int FLAGS, int PACE = 0>
+template <int FLAGS, int PACE = 0, int AHEAD = 6>
 __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     constexpr int NK = 12;
     constexpr bool EMIT = true;
-    constexpr int S = 8, A = 6;
+    constexpr int A = AHEAD, S = AHEAD + 2;  // slices in flight, ring slots
+    static_assert(A >= 4 && A < NK, "lookahead");
     constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
     constexpr int CAP = 10;
     constexpr int EM_BYTES = NT * 2 * CAP * 8;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     } else {
         for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
     }
-    qs_barrier((FLAGS & kNoDma) ? 0 : (pre >= 3 ? pre - 3 : 0));
+    qs_barrier((FLAGS & kNoDma) ? 0 : (pre >= 3 ? pre - 3 : 0));  // slices 0..2 landed
     if (J)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) fa[rb] = *reinterpret_cast<const i32x4v_t*>(lds + rb * 1024 + aoff0);
@@ -184,7 +185,9 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
                     if (FLAGS & kNoBar) {
                         if (!(FLAGS & kNoDma)) qs_wait_n_nobar(2 + (kt <= 2 ? 1 : 0));
                     } else {
-                        qs_wait_n((FLAGS & kNoDma) ? (kt <= 2 ? 1 : 0) : 2 + (kt <= 2 ? 1 : 0));
+                        // slices <= jj + 3 landed: the A - 4 younger slices' DMAs (and the tile's
+                        // scale load while it is younger than slice jj + 3's, kt <= A - 4) in flight
+                        qs_wait_n((FLAGS & kNoDma) ? (kt <= A - 4 ? 1 : 0) : (A - 4) + (kt <= A - 4 ? 1 : 0));
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);

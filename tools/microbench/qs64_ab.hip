@@ -73,9 +73,9 @@ int main(int argc, char** argv) {
         {"qs64 (1 wave/SIMD, lab)", bsrlab::k_filter_qs64<12>, 256, {}},
         {"qs16x static-dma", k_qs16x<kStaticDma>, 512, {}},
         {"qs16x copy", k_qs16x<0>, 512, {}},
-        {"sdma pace 2", k_qs16x<kStaticDma, 2>, 512, {}},
-        {"sdma pace 4", k_qs16x<kStaticDma, 4>, 512, {}},
-        {"sdma pace 8", k_qs16x<kStaticDma, 8>, 512, {}},
+        {"sdma ahead 5", k_qs16x<kStaticDma, 0, 5>, 512, {}},
+        {"sdma ahead 7", k_qs16x<kStaticDma, 0, 7>, 512, {}},
+        {"sdma ahead 8", k_qs16x<kStaticDma, 0, 8>, 512, {}},
     };
     const size_t n_main = vs.size();
     // timing-only ablations (outputs not compared)

@@ -33,7 +33,8 @@ def main():
     write = per_kernel(wdir, "WRITE_SIZE")
     # the emitting filter with the largest fetch (the skinny single-query filter matches too)
     emit = sorted((k for k in fetch if "k_filter" in k and "true" in k), key=lambda k: -fetch[k])
-    res = {"rows": int(rows), "queries": int(queries), "filter": filt, "kernels": {}}
+    res = {"rows": int(rows), "queries": int(queries), "filter": filt, "run": os.environ.get("PMC_RUN", ""),
+           "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k)
         w = write.get(k)
