@@ -13,10 +13,13 @@
 //   kNoLdsRead   no fragment reads (the MFMAs reuse the fragments in registers: timing only)
 //   kSameTile    every row tile's DMA reads the workgroup's FIRST tile (always L2-resident: the
 //                upside of perfect L2 sharing among the workgroups of a row-tile stream)
+//   kSliceMajor  (with kStaticDma) the operand stored slice-major inside each 128-row tile:
+//                tile rt = NK slices of 128 rows x 64 B, each slice one contiguous 8 KiB
+//                (product: row-major, a slice = 128 half-lines 768 B apart)
 namespace bsrlab {
 using namespace bsr;
 
-enum : int { kStaticDma = 1, kNoEpi = 2, kNoBar = 4, kNoDma = 8, kNoLdsRead = 16, kSameTile = 32 };
+enum : int { kStaticDma = 1, kNoEpi = 2, kNoBar = 4, kNoDma = 8, kNoLdsRead = 16, kSameTile = 32, kSliceMajor = 64 };
 // PACE > 0: the n_qt workgroups that stream the same row tiles (same g0) keep within PACE
 // tiles of each other: after each tile wave 0 publishes its count (relaxed agent-scope store,
 // progress words in p.S, zeroed before the launch); before each tile it reads the group's
@@ -81,7 +84,9 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
 
     const uint32_t lrow = w * 16 + (lane >> 2);
     const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
-    const uint32_t aoff_dma = lrow * (uint32_t)p.a_stride + lchunk;
+    constexpr bool SM = (FLAGS & kSliceMajor) != 0;
+    constexpr uint32_t kSliceSrc = SM ? BM * kSliceB : kSliceB;  // source bytes between slices
+    const uint32_t aoff_dma = lrow * (SM ? (uint32_t)kSliceB : (uint32_t)p.a_stride) + lchunk;
     auto rsrc_for = [&](uint32_t ti) {
         const uint32_t rt = g0 + ((FLAGS & kSameTile) ? 0 : ti) * RG;
         return __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
@@ -106,9 +111,9 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
         if (FLAGS & kNoDma) return;
         uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
         if (kt + A < NK)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, aoff_dma, (kt + A) * kSliceB, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, aoff_dma, (kt + A) * kSliceSrc, 0, 0);
         else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_nxt, (lds_void_t*)la, 16, aoff_dma, (kt + A - NK) * kSliceB, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_nxt, (lds_void_t*)la, 16, aoff_dma, (kt + A - NK) * kSliceSrc, 0, 0);
     };
     const uint32_t aoff0 = (lane & 15) * kSliceB + (((lane >> 4) ^ qs16_swz(lane & 15)) * 16);
     i32x4v_t fa[4];
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
         if (!(FLAGS & kNoDma))
             for (uint32_t jj = 0; jj < pre; ++jj) {
                 uint8_t* la = lds + (jj % S) * SLOT + wu * 1024;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, aoff_dma, jj * kSliceB, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_cur, (lds_void_t*)la, 16, aoff_dma, jj * kSliceSrc, 0, 0);
             }
     } else {
         for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);

@@ -31,6 +31,14 @@ __global__ void fill_i8(int8_t* p, size_t n, uint64_t seed) {
         p[i] = (int8_t)((int)(h % 255) - 127);
     }
 }
+// slice-major copy of a row-major int8 operand: tile t (128 rows) = 12 slices of 128 x 64 B
+__global__ void to_slice_major(const uint8_t* a, uint8_t* o, size_t npad) {
+    const size_t n16 = npad * 768 / 16;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = i / 48, c = i % 48, t = row / 128, r = row % 128, s = c / 4, h = c % 4;
+        reinterpret_cast<uint4*>(o)[(t * 128 * 768 + s * 128 * 64 + r * 64 + h * 16) / 16] = reinterpret_cast<const uint4*>(a)[i];
+    }
+}
 __global__ void fill_f32(float* p, size_t n, float v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -40,12 +48,13 @@ int main(int argc, char** argv) {
     const int rounds = argc > 3 ? atoi(argv[3]) : 20;
     const float tau_emit = argc > 4 ? atof(argv[4]) : 0.125f;
     const uint32_t ld = 768, qpad = (nq + 255) / 256 * 256, npad = (n + 255) / 256 * 256, cap = 1024;
-    uint8_t *A8, *B8;
+    uint8_t *A8, *B8, *A8s;
     float *tau, *as, *bs;
     uint64_t* cand;
     uint32_t* cnt;
     CHECK(hipMalloc(&A8, (size_t)npad * ld));
     CHECK(hipMalloc(&B8, (size_t)qpad * ld));
+    CHECK(hipMalloc(&A8s, (size_t)npad * ld));
     CHECK(hipMalloc(&as, npad / 32 * 4));
     CHECK(hipMalloc(&bs, qpad * 4));
     CHECK(hipMalloc(&tau, qpad * 4));
@@ -54,6 +63,7 @@ int main(int argc, char** argv) {
     uint32_t* prog;  // pacing progress words (lab), zeroed before every launch
     CHECK(hipMalloc(&prog, 4096 * 4));
     hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
+    hipLaunchKernelGGL(to_slice_major, dim3(4096), dim3(256), 0, 0, A8, A8s, (size_t)npad);
     hipLaunchKernelGGL(fill_i8, dim3(1024), dim3(256), 0, 0, (int8_t*)B8, (size_t)qpad * ld, 4);
     hipLaunchKernelGGL(fill_f32, dim3(256), dim3(256), 0, 0, as, (size_t)npad / 32, 1.0f / (127.0f * 16.0f));
     hipLaunchKernelGGL(fill_f32, dim3(16), dim3(256), 0, 0, bs, (size_t)qpad, 1.0f / (127.0f * 16.0f));
@@ -66,7 +76,7 @@ int main(int argc, char** argv) {
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
 
-    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; };
+    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; };
     using namespace bsrlab;
     std::vector<V> vs = {
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, 512, {}},
@@ -76,6 +86,9 @@ int main(int argc, char** argv) {
         {"sdma ahead 5", k_qs16x<kStaticDma, 0, 5>, 512, {}},
         {"sdma ahead 7", k_qs16x<kStaticDma, 0, 7>, 512, {}},
         {"sdma ahead 8", k_qs16x<kStaticDma, 0, 8>, 512, {}},
+        {"slice-major", k_qs16x<kStaticDma | kSliceMajor>, 512, {}, true},
+        {"slice-major ahd 4", k_qs16x<kStaticDma | kSliceMajor, 0, 4>, 512, {}, true},
+        {"slice-major ahd 8", k_qs16x<kStaticDma | kSliceMajor, 0, 8>, 512, {}, true},
     };
     const size_t n_main = vs.size();
     // timing-only ablations (outputs not compared)
@@ -88,6 +101,7 @@ int main(int argc, char** argv) {
         {"x no-epi no-dma/rd", k_qs16x<kNoEpi | kNoDma | kNoLdsRead>, 512, {}},
         {"x no-epi/dma/rd/bar", k_qs16x<kNoEpi | kNoDma | kNoLdsRead | kNoBar>, 512, {}},
         {"x sdma same-tile", k_qs16x<kStaticDma | kSameTile>, 512, {}},
+        {"x sm no-epi", k_qs16x<kStaticDma | kSliceMajor | kNoEpi>, 512, {}, true},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
@@ -97,8 +111,10 @@ int main(int argc, char** argv) {
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
         CHECK(hipMemset(cnt, 0, qpad * 4));
         CHECK(hipMemset(prog, 0, 4096 * 4));
+        bsr::GemmArgs gv = g;
+        if (v.sm) gv.A = A8s;
         CHECK(hipEventRecord(e0));
-        hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, g);
+        hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, gv);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
