@@ -82,8 +82,23 @@ __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 // certification, every emitted row (~4k'), their count read on the device
 // (a.n_items_dev), so the launch needs no host round trip.  P chunks of candidate rows are
 // loaded ahead (rows of 768 floats; other widths: 2).
+#ifdef BSR_RESCORE_STAMPS
+// (lab build only: per-wave phase timestamps of the one-wave-per-query rescore, 100 MHz clock)
+__device__ uint64_t g_rescore_stamps[4096 * 8];
+#define BSR_STAMP(W_, I_)                                                                          \
+    do {                                                                                           \
+        if ((W_) == 1 && threadIdx.x == 0 && blockIdx.x < 4096)                                    \
+            g_rescore_stamps[blockIdx.x * 8 + (I_)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#else
+#define BSR_STAMP(W_, I_) \
+    do {                  \
+    } while (0)
+#endif
+
 template <int E, int W, int P>
 __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
+    BSR_STAMP(W, 0);
     constexpr int STAGE = 64 * 68;  // 64 rows (stride 68) per wave
     constexpr int QMAX = 1024;      // the whole query in LDS (rows up to 1024 floats)
     __shared__ __attribute__((aligned(16))) float lds_all[W * STAGE + QMAX];
@@ -101,18 +116,49 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     }
     for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
         const uint32_t q = a.qlist ? a.qlist[item] : item;
-        // the query, once per item (its loads are not behind the candidate prefetch); rows
-        // longer than QMAX read it from global memory instead
-        const bool qlds = a.ld <= (uint32_t)QMAX;
-        if (qlds)
-            for (uint32_t c = threadIdx.x; c < a.ld; c += 64 * W) ldq_all[c] = a.qf32[(uint64_t)q * a.ld + c];
-        if constexpr (W > 1) __syncthreads();
-        else wave_sync();
         // mode S (a.sel: select the k' candidates here, from the emitted keys), mode B (every
         // emitted candidate) or mode A (the k' selected ones, from k_select_cand)
         const bool sel = W == 1 && a.sel;
         const bool all = !sel && a.cand_keys != nullptr;
+        // The item's independent loads are all issued before any is consumed -- the candidate
+        // count, the emitted keys (mode S: every one of the cap <= 1024 slots, masked by the
+        // count afterwards, so they do not wait for it) and the query row in one batch.  (Phase
+        // stamps, tools/diag/rescore_stamps.py: query + keys 7.2 -> 5.5 us of a 46-48 us wave;
+        // the rows' scan that follows is HBM-bound, ~31 us for 63k rows at 1000 queries.)
         const uint32_t cnt = (sel || all) ? a.cnt[q] : a.ncand[q];
+        constexpr int NR = 16;
+        uint64_t xk[W == 1 ? NR : 1];
+        if constexpr (W == 1) {
+            if (sel) {
+                const uint64_t* src = a.cand_keys + (uint64_t)q * a.cap;
+#pragma unroll
+                for (int j = 0; j < NR; ++j) {
+                    const uint32_t i = j * kWave + lane;
+                    xk[j] = i < a.cap ? src[i] : kKeyNone;
+                }
+            }
+        }
+        // the query, once per item (its loads are not behind the candidate prefetch); rows
+        // longer than QMAX read it from global memory instead
+        const bool qlds = a.ld <= (uint32_t)QMAX;
+        if (qlds) {
+            constexpr int QN = QMAX / (64 * W);
+            const float* qsrc = a.qf32 + (uint64_t)q * a.ld;
+            float qv[QN];
+#pragma unroll
+            for (int j = 0; j < QN; ++j) {
+                const uint32_t cc = j * 64 * W + threadIdx.x;
+                qv[j] = cc < a.ld ? qsrc[cc] : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < QN; ++j) {
+                const uint32_t cc = j * 64 * W + threadIdx.x;
+                if (cc < a.ld) ldq_all[cc] = qv[j];
+            }
+        }
+        if constexpr (W > 1) __syncthreads();
+        else wave_sync();
+        BSR_STAMP(W, 1);
         const bool overflow = (sel || all) && cnt > a.cap;  // rows were dropped: nothing can be certified
         uint32_t c = overflow ? 0u : cnt;
         float tx_sel = INFINITY;
@@ -120,13 +166,11 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         if (W == 1 && sel) {
             // the (kp+1)-th smallest key T by radix select over the emitted keys (cap <= 1024:
             // 16 registers), the kp keys below it compacted through LDS; kp <= 63 (one pass)
-            constexpr int NR = 16;
-            const uint64_t* src = a.cand_keys + (uint64_t)q * a.cap;
             uint64_t x[NR];
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
                 const uint32_t i = j * kWave + lane;
-                x[j] = i < c ? src[i] : kKeyNone;
+                x[j] = i < c ? xk[j] : kKeyNone;
             }
             uint64_t T = kKeyNone;
             if (!overflow && c > a.kp) {
@@ -205,6 +249,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             sel_row = lane < (int)c ? lsel[lane] : 0u;
             wave_sync();
         }
+        BSR_STAMP(W, 2);
         const float mag_b = a.nb[q];
         const uint32_t ld = a.ld, dim = a.dim, nch = ld / 64;
         const float* rows = a.rows;
@@ -270,6 +315,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         if (qlds && nch == 12) scan(std::true_type{}, std::integral_constant<uint32_t, 12>{});
         else if (qlds) scan(std::true_type{}, std::integral_constant<uint32_t, 0>{});
         else scan(std::false_type{}, std::integral_constant<uint32_t, 0>{});
+        BSR_STAMP(W, 3);
         if constexpr (W > 1) {
             // the W lists (k <= 64E keys each) through LDS, merged by wave 0
             static_assert(W * 64 * E * 8 <= (int)sizeof(lds_all), "merge area");
@@ -335,6 +381,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                 if (lane == 0) a.res_cnt[q] = cnt;
             }
         }
+        BSR_STAMP(W, 4);
     }
 }
 
@@ -674,6 +721,11 @@ __global__ void k_cosine_pair(const float* __restrict__ a, uint32_t la, const fl
 // ------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------
+#ifdef BSR_RESCORE_STAMPS
+extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rescore_stamps), (size_t)n * 8 * sizeof(uint64_t));
+}
+#endif
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     if (!a.n_items) return hipSuccess;
     const uint32_t e = (a.k + 63) / 64;
