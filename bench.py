@@ -135,8 +135,6 @@ def run_c1(args):
     qdev = torch.empty((Q, D), dtype=torch.float32, device=dev)
     bsr.synth_uniform(qdev.data_ptr(), 0, Q, D, 43)
     bsr.synth_uniform(qdev[0:1].data_ptr(), 0, 1, D, 42)
-    if corpus_bf16:  # the corpus holds row 0's bf16 rounding: query 0 is that row exactly
-        qdev[0:1] = qdev[0:1].to(torch.bfloat16).to(torch.float32)
     torch.cuda.synchronize()
     rows_h, q_h = corpus.cpu().numpy(), qdev.cpu().numpy()
     del corpus
