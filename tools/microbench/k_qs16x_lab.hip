@@ -35,12 +35,15 @@ __device__ __forceinline__ void qs_wait_n_nobar(int n) {
     else wait_vm_only<2>();
 }
 
-template <int FLAGS, int PACE = 0, int AHEAD = 6>
+// BP: slices per barrier (product 2).  Ring slots S = AHEAD + BP; at the barrier of slice jj
+// (jj % BP == BP - 1, mid-slice) slices <= jj + BP + 1 must have landed, so AHEAD - BP - 2
+// younger slices stay in flight.
+template <int FLAGS, int PACE = 0, int AHEAD = 6, int BP = 2>
 __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     constexpr int NK = 12;
     constexpr bool EMIT = true;
-    constexpr int A = AHEAD, S = AHEAD + 2;  // slices in flight, ring slots
-    static_assert(A >= 4 && A < NK, "lookahead");
+    constexpr int A = AHEAD, S = AHEAD + BP;  // slices in flight, ring slots
+    static_assert(A >= BP + 2 && A < NK && NK % BP == 0, "lookahead");
     constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
     constexpr int CAP = 10;
     constexpr int EM_BYTES = NT * 2 * CAP * 8;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
     } else {
         for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
     }
-    qs_barrier((FLAGS & kNoDma) ? 0 : (pre >= 3 ? pre - 3 : 0));  // slices 0..2 landed
+    qs_barrier((FLAGS & kNoDma) ? 0 : (pre >= (uint32_t)BP + 1 ? pre - (BP + 1) : 0));  // slices 0..BP landed
     if (J)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) fa[rb] = *reinterpret_cast<const i32x4v_t*>(lds + rb * 1024 + aoff0);
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
 #pragma unroll
         for (int kt = 0; kt < NK; ++kt) {
             const uint32_t jj = t * NK + kt;
-            const bool bar_slice = (kt & 1) == 1;
+            const bool bar_slice = (kt % BP) == BP - 1;
 #pragma unroll
             for (int rb = 0; rb < 8; ++rb) {
 #pragma unroll
@@ -192,7 +195,8 @@ __global__ __launch_bounds__(512, 1) void k_qs16x(GemmArgs p) {
                     } else {
                         // slices <= jj + 3 landed: the A - 4 younger slices' DMAs (and the tile's
                         // scale load while it is younger than slice jj + 3's, kt <= A - 4) in flight
-                        qs_wait_n((FLAGS & kNoDma) ? (kt <= A - 4 ? 1 : 0) : (A - 4) + (kt <= A - 4 ? 1 : 0));
+                        qs_wait_n((FLAGS & kNoDma) ? (kt <= A - BP - 2 ? 1 : 0)
+                                                   : (A - BP - 2) + (kt <= A - BP - 2 ? 1 : 0));
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);

@@ -80,28 +80,20 @@ int main(int argc, char** argv) {
     using namespace bsrlab;
     std::vector<V> vs = {
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, 512, {}},
-        {"qs64 (1 wave/SIMD, lab)", bsrlab::k_filter_qs64<12>, 256, {}},
         {"qs16x static-dma", k_qs16x<kStaticDma>, 512, {}},
-        {"qs16x copy", k_qs16x<0>, 512, {}},
-        {"sdma ahead 5", k_qs16x<kStaticDma, 0, 5>, 512, {}},
-        {"sdma ahead 7", k_qs16x<kStaticDma, 0, 7>, 512, {}},
-        {"sdma ahead 8", k_qs16x<kStaticDma, 0, 8>, 512, {}},
-        {"slice-major", k_qs16x<kStaticDma | kSliceMajor>, 512, {}, true},
-        {"slice-major ahd 4", k_qs16x<kStaticDma | kSliceMajor, 0, 4>, 512, {}, true},
-        {"slice-major ahd 8", k_qs16x<kStaticDma | kSliceMajor, 0, 8>, 512, {}, true},
+        {"bar/3 ahead 7", k_qs16x<kStaticDma, 0, 7, 3>, 512, {}},
+        {"bar/3 ahead 6", k_qs16x<kStaticDma, 0, 6, 3>, 512, {}},
+        {"bar/2 ahead 7", k_qs16x<kStaticDma, 0, 7, 2>, 512, {}},
     };
     const size_t n_main = vs.size();
     // timing-only ablations (outputs not compared)
     std::vector<V> abl = {
         {"x no-epi", k_qs16x<kNoEpi>, 512, {}},
         {"x sdma no-epi", k_qs16x<kStaticDma | kNoEpi>, 512, {}},
-        {"x no-epi no-bar", k_qs16x<kNoEpi | kNoBar>, 512, {}},
-        {"x no-epi no-dma", k_qs16x<kNoEpi | kNoDma>, 512, {}},
-        {"x no-epi no-ldsrd", k_qs16x<kNoEpi | kNoLdsRead>, 512, {}},
+        {"x bar/3 no-epi", k_qs16x<kStaticDma | kNoEpi, 0, 7, 3>, 512, {}},
         {"x no-epi no-dma/rd", k_qs16x<kNoEpi | kNoDma | kNoLdsRead>, 512, {}},
+        {"x bar/3 no-epi no-dma/rd", k_qs16x<kStaticDma | kNoEpi | kNoDma | kNoLdsRead, 0, 7, 3>, 512, {}},
         {"x no-epi/dma/rd/bar", k_qs16x<kNoEpi | kNoDma | kNoLdsRead | kNoBar>, 512, {}},
-        {"x sdma same-tile", k_qs16x<kStaticDma | kSameTile>, 512, {}},
-        {"x sm no-epi", k_qs16x<kStaticDma | kSliceMajor | kNoEpi>, 512, {}, true},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
