@@ -74,7 +74,7 @@ def _same(r, want):
         assert np.array_equal(r["dist"][q, :c].view(np.uint32), wd[q, :c].view(np.uint32)), q
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_parallel_search_multirank_matches_oracle(bsr_mod, oracle_mod, gpu, corpus, tmp_path, world):
     rows, q = corpus
     res = _run(world, "normal", tmp_path)
