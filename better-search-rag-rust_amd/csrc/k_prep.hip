@@ -312,35 +312,41 @@ __global__ __launch_bounds__(256) void k_rows_to_i8_sample(const float* __restri
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kQueryLdsFloats = 8192;  // rows up to 8192 floats are staged in LDS
 
-__global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, uint32_t nq, uint32_t dim,
-                                                   uint32_t ld, FilterOp op, bool with_op,
-                                                   const uint32_t* __restrict__ ea_max,
-                                                   float* __restrict__ qf32, float* __restrict__ nb,
-                                                   void* __restrict__ qop, float* __restrict__ qscale,
-                                                   float* __restrict__ ebound, uint32_t* __restrict__ qflags,
-                                                   int32_t* __restrict__ qids, uint32_t* __restrict__ status) {
+// Two waves per query: wave 0's lane 0 walks the row for the exact |b| (the reference's
+// dependent chain of f32 adds) while wave 1 quantises it to int8 (double precision) at the
+// same time; the int8 result is kept only if |b| admits the filter (else zeros, E_q = inf).
+__global__ __launch_bounds__(128) void k_query_prep(const float* __restrict__ q, uint32_t nq, uint32_t dim,
+                                                    uint32_t ld, FilterOp op, bool with_op,
+                                                    const uint32_t* __restrict__ ea_max,
+                                                    float* __restrict__ qf32, float* __restrict__ nb,
+                                                    void* __restrict__ qop, float* __restrict__ qscale,
+                                                    float* __restrict__ ebound, uint32_t* __restrict__ qflags,
+                                                    int32_t* __restrict__ qids, uint32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) float row[kQueryLdsFloats];
     __shared__ float s_mag;
     __shared__ uint32_t s_flags;
+    __shared__ uint32_t s_bad;
     const uint32_t qi = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool real = qi < nq;
     const bool staged = ld <= kQueryLdsFloats;
     const float* src = q + (uint64_t)qi * dim;
     float* dst = qf32 + (uint64_t)qi * ld;
+    if (t == 0) s_bad = 0;
+    __syncthreads();
     bool bad = false;
-    // 16 loads per lane in flight, then their stores (rows up to 1024 floats: one round)
-    constexpr int B = 16;
-    for (uint32_t c0 = 0; c0 < ld; c0 += B * kWave) {
+    // 8 loads per thread in flight, then their stores (rows up to 1024 floats: one round)
+    constexpr int B = 8;
+    for (uint32_t c0 = 0; c0 < ld; c0 += B * 128) {
         float v[B];
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            const uint32_t c = c0 + j * kWave + lane;
+            const uint32_t c = c0 + j * 128 + t;
             v[j] = (real && c < dim) ? src[c] : 0.0f;
         }
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            const uint32_t c = c0 + j * kWave + lane;
+            const uint32_t c = c0 + j * 128 + t;
             if (c < ld) {
                 bad |= !isfinite(v[j]);
                 dst[c] = v[j];
@@ -348,9 +354,51 @@ __global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, 
             }
         }
     }
-    bad = __ballot(bad) != 0;
+    if (__ballot(bad) != 0 && lane == 0) s_bad = 1;
     __syncthreads();
-    if (lane == 0) {
+    bad = s_bad != 0;
+    auto val = [&](uint32_t c) -> float { return staged ? row[c] : dst[c]; };
+    const bool i8 = with_op && op != kFilterBF16;
+    // wave 1 (int8 operand): the quantisation, speculatively, into registers
+    constexpr int QV = 4;  // char4 groups per lane held (rows up to 1024 int8); longer rows: second pass
+    char4 qv[QV];
+    double e2 = 0.0;
+    float sc = 1.0f;
+    if (w == 1 && i8) {
+        double ss = 0.0, mx = 0.0;
+        if (real && !bad) {
+            for (uint32_t c = lane; c < dim; c += kWave) {
+                const double x = val(c);
+                ss += x * x;
+                mx = fmax(mx, fabs(x));
+            }
+        }
+        ss = wave_sum_f64(ss);
+        mx = wave_max_f64(mx);
+        const double inv = ss > 0.0 ? 1.0 / sqrt(ss) : 0.0;
+        sc = (mx > 0.0 && inv > 0.0) ? f32_round_up(mx * inv / 127.0) : 1.0f;
+        const double sd = sc;
+        for (uint32_t g = 0, c0 = lane * 4; c0 < ld; ++g, c0 += 4 * kWave) {
+            int8_t qq[4] = {0, 0, 0, 0};
+            if (inv > 0.0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t c = c0 + j;
+                    if (c < dim) {
+                        const double x = (double)val(c) * inv;
+                        qq[j] = quant_i8(x, sd);
+                        const double d = x - sd * (double)qq[j];
+                        e2 += d * d;
+                    }
+                }
+            }
+            const char4 v4 = make_char4(qq[0], qq[1], qq[2], qq[3]);
+            if (g < (uint32_t)QV) qv[g] = v4;
+            else *reinterpret_cast<char4*>(static_cast<int8_t*>(qop) + (uint64_t)qi * ld + c0) = v4;
+        }
+        e2 = wave_sum_f64(e2);
+    }
+    if (t == 0) {
         // the reference's sequential sum, 16 elements per step from 4 ds_read_b128
         float acc = -0.0f;
         uint32_t i = 0;
@@ -382,47 +430,21 @@ __global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ q, 
     __syncthreads();
     const bool ok = !(s_flags & kQueryNoApprox);
     if (!with_op) return;
-    auto val = [&](uint32_t c) -> float { return staged ? row[c] : dst[c]; };
     if (op == kFilterBF16) {
         uint16_t* o = static_cast<uint16_t*>(qop) + (uint64_t)qi * ld;
         const float m = ok ? s_mag : 1.0f;
-        for (uint32_t c = lane; c < ld; c += kWave)
+        for (uint32_t c = t; c < ld; c += 128)
             o[c] = (ok && c < dim) ? f32_to_bf16_rne(val(c) / m) : (uint16_t)0;
-        if (lane == 0) ebound[qi] = ok ? (float)kEBoundBF16 : INFINITY;
+        if (t == 0) ebound[qi] = ok ? (float)kEBoundBF16 : INFINITY;
         return;
     }
+    if (w != 1) return;
+    // wave 1: keep the speculative operand (the filter serves this query) or zero it
     int8_t* o = static_cast<int8_t*>(qop) + (uint64_t)qi * ld;
-    double ss = 0.0, mx = 0.0;
-    if (ok) {
-        for (uint32_t c = lane; c < dim; c += kWave) {
-            const double x = val(c);
-            ss += x * x;
-            mx = fmax(mx, fabs(x));
-        }
+    for (uint32_t g = 0, c0 = lane * 4; c0 < ld; ++g, c0 += 4 * kWave) {
+        if (g < (uint32_t)QV) *reinterpret_cast<char4*>(o + c0) = ok ? qv[g] : make_char4(0, 0, 0, 0);
+        else if (!ok) *reinterpret_cast<char4*>(o + c0) = make_char4(0, 0, 0, 0);
     }
-    ss = wave_sum_f64(ss);
-    mx = wave_max_f64(mx);
-    const double inv = ok && ss > 0.0 ? 1.0 / sqrt(ss) : 0.0;
-    const float sc = (ok && mx > 0.0) ? f32_round_up(mx * inv / 127.0) : 1.0f;
-    const double s = sc;
-    double e2 = 0.0;
-    for (uint32_t c0 = lane * 4; c0 < ld; c0 += 4 * kWave) {
-        int8_t qv[4] = {0, 0, 0, 0};
-        if (ok) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t c = c0 + j;
-                if (c < dim) {
-                    const double x = (double)val(c) * inv;
-                    qv[j] = quant_i8(x, s);
-                    const double d = x - s * (double)qv[j];
-                    e2 += d * d;
-                }
-            }
-        }
-        *reinterpret_cast<char4*>(o + c0) = make_char4(qv[0], qv[1], qv[2], qv[3]);
-    }
-    e2 = wave_sum_f64(e2);
     if (lane == 0) {
         qscale[qi] = ok ? sc : 0.0f;
         if (ok) {
@@ -489,7 +511,7 @@ hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim,
     return hipGetLastError();
 }
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(64), 0, s, a.q, a.nq, a.dim, a.ld, a.op, a.with_op,
+    hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(128), 0, s, a.q, a.nq, a.dim, a.ld, a.op, a.with_op,
                        a.ea_max, a.qf32, a.nb, a.qop, a.qscale, a.ebound, a.qflags, a.qids, a.status);
     return hipGetLastError();
 }
