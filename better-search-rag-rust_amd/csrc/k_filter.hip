@@ -471,6 +471,23 @@ constexpr int kSampleTilesPerWG = 8;  // sample pass (compact): tiles of maxima 
 
 __device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
 
+#ifdef BSR_FILTER_COUNTERS
+// (lab build only: emission-epilogue event counts of k_filter_qs16<true>, summed per wave)
+__device__ unsigned long long g_filter_counters[8];
+extern "C" int bsr_lab_filter_counters(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_filter_counters), sizeof(g_filter_counters));
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_filter_counters), z, sizeof(z));
+    }
+    return (int)e;
+}
+#define BSR_FCNT(I_) ++fcnt[I_]
+#else
+#define BSR_FCNT(I_) \
+    do {             \
+    } while (0)
+#endif
 template <bool EMIT, int NK>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
@@ -591,6 +608,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
 
+#ifdef BSR_FILTER_COUNTERS
+    unsigned long long fcnt[4] = {0, 0, 0, 0};
+#endif
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
         if (kStatic && t) {
@@ -693,6 +713,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
             const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
             const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
             bool any = false;
+            BSR_FCNT(0);
             int mrb[2];  // (unused lanes' values are never read)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
@@ -705,6 +726,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
             }
             if (__ballot(any)) {
+                BSR_FCNT(1);
                 // level 2: per (query block, 16-row block) its maximum against tau -- eight
                 // independent scores, then one uniform branch per passing row block -- and that
                 // block's 4 rows appended without branches (every key is written to the next
@@ -712,6 +734,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
                     if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
+                    BSR_FCNT(2);
                     bool pass_rb[8];
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
@@ -722,6 +745,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
                         if (!__ballot(pass_rb[rb])) continue;
+                        BSR_FCNT(3);
                         if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
                             flush_ring(nb);
                             stored = true;
@@ -745,6 +769,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     if constexpr (EMIT) {
         flush_ring(0);
         flush_ring(1);
+#ifdef BSR_FILTER_COUNTERS
+        if (lane == 0)
+            for (int i = 0; i < 4; ++i) atomicAdd(&g_filter_counters[i], fcnt[i]);
+#endif
     }
 }
 
