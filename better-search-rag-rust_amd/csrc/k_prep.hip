@@ -296,9 +296,9 @@ __global__ __launch_bounds__(256) void k_rows_to_i8_sample(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------
-// Queries: one wave per (padded) query, the whole preparation in one kernel.
+// Queries: one workgroup of two waves per (padded) query, the whole preparation in one kernel.
 //   1. the caller's row -> LDS (coalesced) and the padded f32 copy qf32[q] (zeros past dim)
-//   2. lane 0 walks the row in index order: |b| exactly as src/metrics.rs:155 (sequential
+//   2. wave 0's lane 0 walks the row in index order: |b| exactly as src/metrics.rs:155 (sequential
 //      f32 sum of squares from -0.0, correctly rounded sqrt), finiteness
 //   3. flags, the identity query-id list of the exact scan (min(q, nq-1))
 //   4. the filter operand from the LDS copy:
@@ -312,9 +312,9 @@ __global__ __launch_bounds__(256) void k_rows_to_i8_sample(const float* __restri
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kQueryLdsFloats = 8192;  // rows up to 8192 floats are staged in LDS
 
-// Two waves per query: wave 0's lane 0 walks the row for the exact |b| (the reference's
-// dependent chain of f32 adds) while wave 1 quantises it to int8 (double precision) at the
-// same time; the int8 result is kept only if |b| admits the filter (else zeros, E_q = inf).
+// Steps 2 and 4 (int8) overlap: while wave 0's lane 0 walks the exact |b| (the reference's
+// dependent chain of f32 adds), wave 1 quantises the row to int8 (double precision) into
+// registers; the result is kept only if |b| admits the filter (else zeros, E_q = inf).
 __global__ __launch_bounds__(128) void k_query_prep(const float* __restrict__ q, uint32_t nq, uint32_t dim,
                                                     uint32_t ld, FilterOp op, bool with_op,
                                                     const uint32_t* __restrict__ ea_max,
