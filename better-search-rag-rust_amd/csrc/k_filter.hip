@@ -482,6 +482,11 @@ extern "C" int bsr_lab_filter_counters(unsigned long long* out, int reset) {
     }
     return (int)e;
 }
+// per-workgroup timestamps (100 MHz): [block][0] start (wave 0), [block][1 + w] wave w's end
+__device__ unsigned long long g_filter_wg_stamps[4096 * 9];
+extern "C" int bsr_lab_filter_wg_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_filter_wg_stamps), sizeof(g_filter_wg_stamps));
+}
 #define BSR_FCNT(I_) ++fcnt[I_]
 #else
 #define BSR_FCNT(I_) \
@@ -610,6 +615,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 
 #ifdef BSR_FILTER_COUNTERS
     unsigned long long fcnt[4] = {0, 0, 0, 0};
+    if (EMIT && tid == 0 && blockIdx.x < 4096) g_filter_wg_stamps[blockIdx.x * 9] = __builtin_amdgcn_s_memrealtime();
 #endif
     for (uint32_t t = 0; t < my_rt; ++t) {
         const uint32_t rt = g0 + t * RG;
@@ -770,8 +776,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         flush_ring(0);
         flush_ring(1);
 #ifdef BSR_FILTER_COUNTERS
-        if (lane == 0)
+        if (lane == 0) {
             for (int i = 0; i < 4; ++i) atomicAdd(&g_filter_counters[i], fcnt[i]);
+            if (blockIdx.x < 4096) g_filter_wg_stamps[blockIdx.x * 9 + 1 + w] = __builtin_amdgcn_s_memrealtime();
+        }
 #endif
     }
 }
