@@ -402,7 +402,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     ix->stats.n_candidates = kp;
     BSR_TRY(ix->tau.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(ix->cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
-    BSR_TRY(ix->cnt.ensure((size_t)qpad * sizeof(uint32_t)));
+    BSR_TRY(ix->cnt.ensure(((size_t)qpad + kTailCounters) * sizeof(uint32_t)));  // + the tail counters
     BSR_TRY(ix->cand_rows.ensure((size_t)nq * kp * sizeof(uint32_t)));
     BSR_TRY(ix->ncand.ensure((size_t)nq * sizeof(uint32_t)));
     BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));
@@ -458,6 +458,8 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     g.cand = ix->cand.as<uint64_t>();
     g.cnt = ix->cnt.as<uint32_t>();
     g.cap = cap;
+    // the last 1/kTailDiv of the row tiles are balanced dynamically (k_filter_qs16)
+    g.tail = g.n_qt <= kTailCounters ? ix->cnt.as<uint32_t>() + qpad : nullptr;
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return skinny ? launch_filter_skinny_emit(g, ix->stream, e0, e1)
                       : launch_filter_emit(ix->op, g, ix->stream, e0, e1);

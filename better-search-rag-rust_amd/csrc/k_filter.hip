@@ -484,6 +484,14 @@ extern "C" int bsr_lab_filter_counters(unsigned long long* out, int reset) {
 }
 // per-workgroup timestamps (100 MHz): [block][0] start (wave 0), [block][1 + w] wave w's end
 __device__ unsigned long long g_filter_wg_stamps[4096 * 9];
+__device__ uint32_t g_lab_xcd_xor;  // the row streams of XCD x go to XCD x ^ this
+extern "C" int bsr_lab_set_xcd_xor(uint32_t v) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_lab_xcd_xor), &v, sizeof v);
+}
+__device__ unsigned int g_filter_wg_tiles[4096 * 2];  // [block]: tiles processed, static tiles
+extern "C" int bsr_lab_filter_wg_tiles(unsigned int* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_filter_wg_tiles), sizeof(g_filter_wg_tiles));
+}
 extern "C" int bsr_lab_filter_wg_stamps(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_filter_wg_stamps), sizeof(g_filter_wg_stamps));
 }
@@ -502,8 +510,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
     // SAMPLE, compact: the workgroup's maxima [tile][4][256 queries], written to S at the end
     constexpr int SB_BYTES = EMIT ? 0 : kSampleTilesPerWG * 4 * BN * 4;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES + SB_BYTES];
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES + SB_BYTES + 16];
     float* const sbuf = reinterpret_cast<float*>(lds + S * SLOT + EM_BYTES);
+    // tail tile ids claimed by wave 0, shared with the other waves: [0..1] in the loop, [2..3] prologue
+    uint32_t* const lds_ids = reinterpret_cast<uint32_t*>(lds + S * SLOT + EM_BYTES + SB_BYTES);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
@@ -514,10 +524,36 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     const uint32_t n_rt = (p.n_rows + BM - 1) / BM;
     const bool active = slot < G * p.n_qt;
     const uint32_t qt = active ? slot % p.n_qt : 0;
+#ifdef BSR_FILTER_COUNTERS
+    const uint32_t g0 = (xcd ^ g_lab_xcd_xor) * G + (active ? slot / p.n_qt : 0);  // (lab: remapped streams)
+#else
     const uint32_t g0 = xcd * G + (active ? slot / p.n_qt : 0);
+#endif
     const uint32_t RG = 8 * G;
     const uint32_t my_rt = (active && g0 < n_rt) ? (n_rt - 1 - g0) / RG + 1 : 0;
     const uint32_t J = my_rt * NK;
+    // Tile sequence: the row stream's static tiles g0, g0 + RG, ... below n_st, then (dyn) tail
+    // tiles claimed from this query tile's counter one at a time -- workgroups on faster XCDs
+    // take more of them (the kernel ends with its slowest workgroup; XCD speeds differ by
+    // 4-10%, profiles/r03bb_*).  Tail tiles are read by the n_qt workgroups of different
+    // streams, so they are not shared through one XCD's L2 -- hence a small tail.
+    constexpr uint32_t kEnd = 0xFFFFFFFFu;
+    constexpr bool kStaticSched = NK > A;
+    const bool dyn = EMIT && kStaticSched && p.tail != nullptr && active;
+    const uint32_t n_st = dyn ? n_rt - n_rt / kTailDiv : n_rt;
+    const uint32_t my_static = (active && g0 < n_st) ? (n_st - 1 - g0) / RG + 1 : 0;
+    // (one lane) claim the next tail tile of this query tile: the counter's old value, turned
+    // into a tile id by tail_id() where it is consumed -- not at once, which would wait for the
+    // atomic and, in order, for every DMA in flight.  The address is one the compiler cannot
+    // prove uniform: the atomic optimizer would otherwise aggregate the atomic across the wave
+    // and consume its result immediately.
+    auto claim_raw = [&]() -> uint32_t {
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        return atomicAdd(p.tail + qt + z, 1u);
+    };
+    auto tail_id = [&](uint32_t v) -> uint32_t { return n_st + v < n_rt ? n_st + v : kEnd; };
+    auto claim = [&]() -> uint32_t { return tail_id(claim_raw()); };
 
     // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
     // qt*256 + 32w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
@@ -549,18 +585,18 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     const uint32_t lchunk = ((lane & 3) ^ qs16_swz(lrow)) * 16;
     // Tile ti's descriptor (base = its first row) and this lane's byte offset in it (SAMPLE:
     // tail rows read the last valid row).
-    auto tile_src = [&](uint32_t ti, __amdgpu_buffer_rsrc_t& rs, uint32_t& off) {
-        const uint32_t rt = g0 + ti * RG;
+    auto tile_src_rt = [&](uint32_t rt, __amdgpu_buffer_rsrc_t& rs, uint32_t& off) {
         rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (uint64_t)rt * BM * p.a_stride), 0,
                                                BM * (uint32_t)p.a_stride, 0x00020000);
         const uint32_t r = (EMIT || rt * BM + lrow < p.n_rows) ? lrow : p.n_rows - 1 - rt * BM;
         off = r * (uint32_t)p.a_stride + lchunk;
     };
+    auto tile_src = [&](uint32_t ti, __amdgpu_buffer_rsrc_t& rs, uint32_t& off) { tile_src_rt(g0 + ti * RG, rs, off); };
     // Static schedule (NK > A, every dim of the product): the DMA issued during slice kt of
     // tile t fills slice (kt + A) % NK of tile t (kt + A < NK) or of tile t + 1 -- both
     // descriptors computed once per tile, so a DMA is two instructions and no branch.  Past
     // the last tile the stream re-reads it (steady counted waits; nobody reads those slots).
-    constexpr bool kStatic = NK > A;
+    constexpr bool kStatic = kStaticSched;
     __amdgpu_buffer_rsrc_t rs_cur, rs_nxt;
     uint32_t off_cur = 0, off_nxt = 0;
     auto dma_static = [&](uint32_t jj, int kt) {
@@ -593,12 +629,28 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     };
 
     i32x4v_t acc[8][2];
-    const uint32_t pre = J ? (uint32_t)A : 0u;
-    if (my_rt) {
-        tile_src(0, rsrc_a, aoff_dma);
+    // the first two tiles of the sequence
+    uint32_t cur_id = my_rt ? g0 : kEnd, nxt_id = my_rt > 1 ? g0 + RG : kEnd;
+    if (dyn && my_static < 2) {
+        if (tid == 0) {
+            const uint32_t a0 = my_static ? g0 : claim();
+            lds_ids[2] = a0;
+            lds_ids[3] = a0 == kEnd ? kEnd : claim();
+        }
+        __syncthreads();
+        cur_id = __builtin_amdgcn_readfirstlane(lds_ids[2]);
+        nxt_id = __builtin_amdgcn_readfirstlane(lds_ids[3]);
+    } else if (dyn) {
+        cur_id = g0;
+        nxt_id = g0 + RG;
+    }
+    const bool any_tile = cur_id != kEnd;
+    const uint32_t pre = (dyn ? any_tile : J != 0) ? (uint32_t)A : 0u;
+    if (any_tile) {
+        tile_src_rt(cur_id, rsrc_a, aoff_dma);
         rs_cur = rsrc_a;
         off_cur = aoff_dma;
-        tile_src(my_rt > 1 ? 1 : 0, rs_nxt, off_nxt);
+        tile_src_rt(nxt_id != kEnd ? nxt_id : cur_id, rs_nxt, off_nxt);
     }
     if (kStatic) {
         for (uint32_t jj = 0; jj < pre; ++jj) {
@@ -609,23 +661,32 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         for (uint32_t jj = 0; jj < pre; ++jj) issue_dma(jj);
     }
     qs_barrier(pre >= 3 ? pre - 3 : 0);  // slices 0, 1, 2 landed everywhere
-    if (J)
+    if (any_tile)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) read_frag(0, rb);
 
 #ifdef BSR_FILTER_COUNTERS
-    unsigned long long fcnt[4] = {0, 0, 0, 0};
+    unsigned long long fcnt[5] = {0, 0, 0, 0, 0};
     if (EMIT && tid == 0 && blockIdx.x < 4096) g_filter_wg_stamps[blockIdx.x * 9] = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (uint32_t t = 0; t < my_rt; ++t) {
-        const uint32_t rt = g0 + t * RG;
+    for (uint32_t t = 0; cur_id != kEnd; ++t) {
+        const uint32_t rt = cur_id;
+        BSR_FCNT(4);
         if (kStatic && t) {
             rs_cur = rs_nxt;
             off_cur = off_nxt;
-            tile_src(t + 1 < my_rt ? t + 1 : t, rs_nxt, off_nxt);
+            tile_src_rt(nxt_id != kEnd ? nxt_id : cur_id, rs_nxt, off_nxt);
         }
         float4 scv = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         if (EMIT) scv = *reinterpret_cast<const float4*>(p.a_scale + (uint64_t)rt * (BM / kQuantBlock));
+        // the tile after next: static, or (dyn) claimed now by wave 0 -- its atomic is one more
+        // VMEM op in wave 0's count at the first barrier (kt = 1), complete by the second --
+        // and shared through LDS at kt = 4, read by every wave after the tile
+        uint32_t n2 = (t + 2 < my_static) ? g0 + (t + 2) * RG : kEnd;
+        const bool req = dyn && t + 2 >= my_static && nxt_id != kEnd;
+        uint32_t claimed = 0;
+        if (req && tid == 0) claimed = claim_raw();
+        const int w0_req = (req && w == 0) ? 1 : 0;
         // SAMPLE: one scale for the tile's 128 sampled rows (a scalar load: counted in lgkmcnt,
         // it leaves the DMA stream's vmcnt waits alone)
         float sc_tile = 1.0f;
@@ -648,6 +709,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (rb < 4) read_frag(jj, rb + 4);
                 else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
+                // (the atomic completed at the kt = 3 barrier; the LDS write completes, in order,
+                // before wave 0's next fragment reads are waited for -- well before kt = 5's barrier)
+                if (kt == 4 && rb == 0 && req && tid == 0) lds_ids[t & 1] = tail_id(claimed);
                 // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
                 // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
                 if (bar_slice ? rb == 6 : rb == 1) {
@@ -659,7 +723,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
                 // the tile's scale load.  (Static schedule: also at the last slice -- the
                 // trailing DMAs keep the count steady -- so no branch.)
-                if (bar_slice && rb == 5 && (kStatic || jj + 1 < J)) qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 : 0));
+                if (bar_slice && rb == 5 && (kStatic || jj + 1 < J))
+                    qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -770,6 +835,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
             }
         }
         if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
+        cur_id = nxt_id;
+        nxt_id = req ? __builtin_amdgcn_readfirstlane(lds_ids[t & 1]) : n2;
     }
     wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
     if constexpr (EMIT) {
@@ -779,6 +846,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         if (lane == 0) {
             for (int i = 0; i < 4; ++i) atomicAdd(&g_filter_counters[i], fcnt[i]);
             if (blockIdx.x < 4096) g_filter_wg_stamps[blockIdx.x * 9 + 1 + w] = __builtin_amdgcn_s_memrealtime();
+            if (blockIdx.x < 4096 && w == 0) {
+                g_filter_wg_tiles[blockIdx.x * 2] = (unsigned int)fcnt[4];
+                g_filter_wg_tiles[blockIdx.x * 2 + 1] = my_static;
+            }
         }
 #endif
     }
@@ -998,6 +1069,7 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
     const uint32_t q = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
+    if (q == 0 && t < (int)kTailCounters) cnt[qpad + t] = 0;  // the emit filter's tail counters
     if (q >= qpad) return;
     if (t == 0) cnt[q] = 0;
     if (q >= nq || (qflags[q] & kQueryNoApprox)) {

@@ -97,7 +97,15 @@ struct GemmArgs {
     uint64_t* cand;         // emit: [qpad][cap] score keys
     uint32_t* cnt;          // emit: [qpad] counters
     uint32_t cap;
+    // emit, int8 query-stationary kernel: all but the last 1/kTailDiv of its 128-row tiles go
+    // to the workgroups' row streams round-robin, the rest are claimed one at a time per query
+    // tile from tail[qt] (zeroed by k_select_tau); tail = nullptr: every tile static
+    uint32_t* tail;
 };
+// Dynamic tail of the emit filter: 1/kTailDiv of the row tiles; counters per query tile
+// (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + qt].
+constexpr uint32_t kTailDiv = 8;
+constexpr uint32_t kTailCounters = 64;
 // e0 / e1 (optional): events recorded at the kernel's own dispatch and completion
 // (hipExtLaunchKernel), i.e. its device duration without the stream's launch gaps.
 hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,

@@ -3,7 +3,9 @@ end timestamps (s_memrealtime, 100 MHz) of the lab build (make -C better-search-
 lab-counters -> tools/ab/libbsr_counters.so; run with BSR_LIB pointing at it).  With a static
 tile partition the kernel ends with its slowest workgroup: mean/max of the workgroup times
 is what perfect balancing could recover.
-usage: BSR_LIB=tools/ab/libbsr_counters.so python tools/diag/filter_wg_balance.py [rows]"""
+usage: BSR_LIB=tools/ab/libbsr_counters.so python tools/diag/filter_wg_balance.py [rows] [xcd_xor]
+(xcd_xor: the lab build hands XCD x's row streams to XCD x ^ xcd_xor -- does a slow XCD stay
+slow with other tiles?)"""
 import ctypes
 import os
 import sys
@@ -28,6 +30,8 @@ bsr.synth_uniform(q.data_ptr(), 0, Q, D, 43)
 torch.cuda.synchronize()
 L = bsr.lib()
 L.bsr_lab_filter_wg_stamps.restype = ctypes.c_int
+XOR = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+assert L.bsr_lab_set_xcd_xor(ctypes.c_uint32(XOR)) == 0
 oi, od, oc = np.empty((Q, K), np.uint64), np.empty((Q, K), np.float32), np.empty(Q, np.uint32)
 G = 256  # filter_grid(n_qt = 4)
 runs = []
@@ -41,7 +45,10 @@ for it in range(14):
     start, end = s[:, 0], s[:, 1:].max(axis=1)
     t0 = start.min()
     runs.append(((start - t0) / 100.0, (end - t0) / 100.0))
-print(f"rows {N}, {Q} queries, grid {G}; {len(runs)} launches")
+    tl = np.zeros((4096, 2), np.uint32)
+    assert L.bsr_lab_filter_wg_tiles(tl.ctypes.data_as(ctypes.c_void_p)) == 0
+    tiles = tl[:G].astype(np.int64)
+print(f"rows {N}, {Q} queries, grid {G}; {len(runs)} launches; streams of XCD x on XCD x ^ {XOR}")
 for i, (st, en) in enumerate(runs):
     dur = en - st
     span = en.max()
@@ -54,5 +61,9 @@ xcd, slot = b & 7, b >> 3
 qt = slot % 4
 print("last launch, mean WG time by XCD:", " ".join(f"{dur[xcd == x].mean():.0f}" for x in range(8)))
 print("last launch, mean WG time by query tile:", " ".join(f"{dur[qt == t].mean():.0f}" for t in range(4)))
+tot, stat = tiles[:, 0], tiles[:, 1]
+print(f"last launch, tiles per WG: min {tot.min()} max {tot.max()} | static {stat.min()}-{stat.max()} | "
+      f"tail tiles per WG min {(tot - stat).min()} max {(tot - stat).max()}")
+print("last launch, tail tiles by XCD:", " ".join(f"{(tot - stat)[xcd == x].mean():.1f}" for x in range(8)))
 srt = np.argsort(dur)[::-1][:8]
 print("slowest WGs (block: us):", ", ".join(f"{int(i)}: {dur[i]:.0f}" for i in srt))

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&bs, qpad * 4));
     CHECK(hipMalloc(&tau, qpad * 4));
     CHECK(hipMalloc(&cand, (size_t)qpad * cap * 8));
-    CHECK(hipMalloc(&cnt, qpad * 4));
+    CHECK(hipMalloc(&cnt, (qpad + bsr::kTailCounters) * 4));
     uint32_t* prog;  // pacing progress words (lab), zeroed before every launch
     CHECK(hipMalloc(&prog, 4096 * 4));
     hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
@@ -76,10 +76,11 @@ int main(int argc, char** argv) {
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
 
-    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; };
+    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; bool tail = false; };
     using namespace bsrlab;
     std::vector<V> vs = {
         {"qs16 (product)", bsr::k_filter_qs16<true, 12>, 512, {}},
+        {"qs16 + dynamic tail", bsr::k_filter_qs16<true, 12>, 512, {}, false, true},
         {"qs16x static-dma", k_qs16x<kStaticDma>, 512, {}},
         {"bar/3 ahead 7", k_qs16x<kStaticDma, 0, 7, 3>, 512, {}},
         {"bar/3 ahead 6", k_qs16x<kStaticDma, 0, 6, 3>, 512, {}},
@@ -101,10 +102,11 @@ int main(int argc, char** argv) {
     auto run = [&](const V& v, float tv) -> float {
         std::vector<float> ht(qpad, tv);
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
-        CHECK(hipMemset(cnt, 0, qpad * 4));
+        CHECK(hipMemset(cnt, 0, (qpad + bsr::kTailCounters) * 4));
         CHECK(hipMemset(prog, 0, 4096 * 4));
         bsr::GemmArgs gv = g;
         if (v.sm) gv.A = A8s;
+        if (v.tail) gv.tail = cnt + qpad;
         CHECK(hipEventRecord(e0));
         hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, gv);
         CHECK(hipEventRecord(e1));
