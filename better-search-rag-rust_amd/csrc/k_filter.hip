@@ -465,6 +465,17 @@ __device__ __forceinline__ void qs_wait_n(int n) {
 #undef BSR_QS_N
 }
 
+#ifdef BSR_FILTER_STAMPS
+__device__ __forceinline__ void qs_vm_n(int n) {  // (stamp build) s_waitcnt vmcnt(n) alone
+#define BSR_QS_V(N) \
+    case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    switch (n) {
+        BSR_QS_V(1) BSR_QS_V(2) BSR_QS_V(3) BSR_QS_V(4) BSR_QS_V(5) BSR_QS_V(6) BSR_QS_V(7) BSR_QS_V(8)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef BSR_QS_V
+}
+#endif
 typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
 
 constexpr int kSampleTilesPerWG = 8;  // sample pass (compact): tiles of maxima staged in LDS
@@ -499,6 +510,27 @@ extern "C" int bsr_lab_filter_wg_stamps(unsigned long long* out) {
 #else
 #define BSR_FCNT(I_) \
     do {             \
+    } while (0)
+#endif
+#ifdef BSR_FILTER_STAMPS
+// (lab build only: s_memtime phase sums of k_filter_qs16<true>, summed over all waves:
+// [0] level-1 epilogue, [1] level-2 epilogue, [2] level-2 entries, [3] the first barrier after
+// the epilogue (kt = 1), [4] the other barriers, [5] loop total, [6] the DMA (vmcnt) waits
+// before the barriers, [7] tiles)
+__device__ unsigned long long g_filter_stamps[8];
+extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_filter_stamps), sizeof(g_filter_stamps));
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_filter_stamps), z, sizeof(z));
+    }
+    return (int)e;
+}
+#define BSR_FST(V_)                                                                     \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(V_)::"memory");       \
+        __builtin_amdgcn_sched_barrier(0);                                              \
     } while (0)
 #endif
 template <bool EMIT, int NK>
@@ -577,6 +609,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 if (gp + i < p.cap) p.cand[(uint64_t)qq[nb] * p.cap + gp + i] = lkeys[(nb * CAP + i) * NT];
         }
         ecnt[nb] = 0;
+        // vmcnt(0) as the builtin (not asm), so that the compiler's wait counting sees the
+        // atomic's return complete on this path: otherwise every join after a flush branch
+        // (each level-2 append) carries a vmcnt(0) that drains the whole DMA stream
+        __builtin_amdgcn_s_waitcnt(0x0F70);
     };
 
     // LDS-DMA: wave w fills rows 16w .. 16w+15 of each slice (1 KiB per instruction); the
@@ -669,6 +705,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     unsigned long long fcnt[5] = {0, 0, 0, 0, 0};
     if (EMIT && tid == 0 && blockIdx.x < 4096) g_filter_wg_stamps[blockIdx.x * 9] = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef BSR_FILTER_STAMPS
+    unsigned long long fst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_a, st_b, st_loop0;
+    BSR_FST(st_loop0);
+#endif
     for (uint32_t t = 0; cur_id != kEnd; ++t) {
         const uint32_t rt = cur_id;
         BSR_FCNT(4);
@@ -723,8 +763,23 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 // DMAs of slices jj + 4, jj + 5 and, while younger than slice jj + 3 (kt <= 2),
                 // the tile's scale load.  (Static schedule: also at the last slice -- the
                 // trailing DMAs keep the count steady -- so no branch.)
-                if (bar_slice && rb == 5 && (kStatic || jj + 1 < J))
+                if (bar_slice && rb == 5 && (kStatic || jj + 1 < J)) {
+#ifdef BSR_FILTER_STAMPS
+                    // (stamp build: the vmcnt wait and the barrier timed apart, [3]/[4] the
+                    // barrier alone, [6] the DMA wait)
+                    if (EMIT) {
+                        BSR_FST(st_a);
+                        qs_vm_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
+                        BSR_FST(st_b);
+                        fst[6] += st_b - st_a;
+                        st_a = st_b;
+                        asm volatile("s_barrier" ::: "memory");
+                        BSR_FST(st_b);
+                        fst[kt == 1 ? 3 : 4] += st_b - st_a;
+                    } else
+#endif
                     qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -785,6 +840,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
             const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
             bool any = false;
             BSR_FCNT(0);
+#ifdef BSR_FILTER_STAMPS
+            BSR_FST(st_a);
+            fst[7] += 1;
+#endif
             int mrb[2];  // (unused lanes' values are never read)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
@@ -796,7 +855,13 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 mrb[nb] = m;
                 any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
             }
-            if (__ballot(any)) {
+            const bool l2 = __ballot(any) != 0;
+#ifdef BSR_FILTER_STAMPS
+            BSR_FST(st_b);
+            fst[0] += st_b - st_a;
+            st_a = st_b;
+#endif
+            if (l2) {
                 BSR_FCNT(1);
                 // level 2: per (query block, 16-row block) its maximum against tau -- eight
                 // independent scores, then one uniform branch per passing row block -- and that
@@ -806,16 +871,16 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 for (int nb = 0; nb < 2; ++nb) {
                     if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
                     BSR_FCNT(2);
-                    bool pass_rb[8];
+                    uint32_t pm = 0;  // the lane's passing row blocks
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
                         const i32x4v_t& x = acc[rb][nb];
                         const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
-                        pass_rb[rb] = ((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb];
+                        pm |= (((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb]) ? 1u << rb : 0u;
                     }
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
-                        if (!__ballot(pass_rb[rb])) continue;
+                        if (!__ballot((pm >> rb) & 1u)) continue;
                         BSR_FCNT(3);
                         if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
                             flush_ring(nb);
@@ -832,6 +897,11 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                         }
                     }
                 }
+#ifdef BSR_FILTER_STAMPS
+                BSR_FST(st_b);
+                fst[1] += st_b - st_a;
+                fst[2] += 1;
+#endif
             }
         }
         if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
@@ -839,6 +909,14 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         nxt_id = req ? __builtin_amdgcn_readfirstlane(lds_ids[t & 1]) : n2;
     }
     wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
+#ifdef BSR_FILTER_STAMPS
+    if (EMIT) {
+        BSR_FST(st_b);
+        fst[5] = st_b - st_loop0;
+        if (lane == 0)
+            for (int i = 0; i < 8; ++i) atomicAdd(&g_filter_stamps[i], fst[i]);
+    }
+#endif
     if constexpr (EMIT) {
         flush_ring(0);
         flush_ring(1);

@@ -79,22 +79,12 @@ int main(int argc, char** argv) {
     struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; bool tail = false; };
     using namespace bsrlab;
     std::vector<V> vs = {
-        {"qs16 (product)", bsr::k_filter_qs16<true, 12>, 512, {}},
-        {"qs16 + dynamic tail", bsr::k_filter_qs16<true, 12>, 512, {}, false, true},
-        {"qs16x static-dma", k_qs16x<kStaticDma>, 512, {}},
-        {"bar/3 ahead 7", k_qs16x<kStaticDma, 0, 7, 3>, 512, {}},
-        {"bar/3 ahead 6", k_qs16x<kStaticDma, 0, 6, 3>, 512, {}},
-        {"bar/2 ahead 7", k_qs16x<kStaticDma, 0, 7, 2>, 512, {}},
+        {"qs16 + tail (product)", bsr::k_filter_qs16<true, 12>, 512, {}, false, true},
     };
     const size_t n_main = vs.size();
     // timing-only ablations (outputs not compared)
     std::vector<V> abl = {
-        {"x no-epi", k_qs16x<kNoEpi>, 512, {}},
         {"x sdma no-epi", k_qs16x<kStaticDma | kNoEpi>, 512, {}},
-        {"x bar/3 no-epi", k_qs16x<kStaticDma | kNoEpi, 0, 7, 3>, 512, {}},
-        {"x no-epi no-dma/rd", k_qs16x<kNoEpi | kNoDma | kNoLdsRead>, 512, {}},
-        {"x bar/3 no-epi no-dma/rd", k_qs16x<kStaticDma | kNoEpi | kNoDma | kNoLdsRead, 0, 7, 3>, 512, {}},
-        {"x no-epi/dma/rd/bar", k_qs16x<kNoEpi | kNoDma | kNoLdsRead | kNoBar>, 512, {}},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
