@@ -25,6 +25,12 @@
         }                                                              \
     } while (0)
 
+__global__ void fill_i8r(int8_t* p, size_t n, uint64_t seed, int r) {  // uniform in [-r, r]
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t h = bsr::splitmix64(seed + i);
+        p[i] = (int8_t)((int)(h % (2 * r + 1)) - r);
+    }
+}
 __global__ void fill_i8(int8_t* p, size_t n, uint64_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t h = bsr::splitmix64(seed + i);
@@ -63,7 +69,12 @@ int main(int argc, char** argv) {
     uint32_t* prog;  // pacing progress words (lab), zeroed before every launch
     CHECK(hipMalloc(&prog, 4096 * 4));
     hipLaunchKernelGGL(fill_i8, dim3(4096), dim3(256), 0, 0, (int8_t*)A8, (size_t)npad * ld, 3);
-    hipLaunchKernelGGL(to_slice_major, dim3(4096), dim3(256), 0, 0, A8, A8s, (size_t)npad);
+    // (A8s: the same corpus at half the integer range, |q| <= 63 -- does the MFMA's operand
+    // range move the clock the chip holds?)
+    hipLaunchKernelGGL(fill_i8r, dim3(4096), dim3(256), 0, 0, (int8_t*)A8s, (size_t)npad * ld, 3, 63);
+    uint8_t* B8n;
+    CHECK(hipMalloc(&B8n, (size_t)qpad * ld));
+    hipLaunchKernelGGL(fill_i8r, dim3(1024), dim3(256), 0, 0, (int8_t*)B8n, (size_t)qpad * ld, 4, 63);
     hipLaunchKernelGGL(fill_i8, dim3(1024), dim3(256), 0, 0, (int8_t*)B8, (size_t)qpad * ld, 4);
     hipLaunchKernelGGL(fill_f32, dim3(256), dim3(256), 0, 0, as, (size_t)npad / 32, 1.0f / (127.0f * 16.0f));
     hipLaunchKernelGGL(fill_f32, dim3(16), dim3(256), 0, 0, bs, (size_t)qpad, 1.0f / (127.0f * 16.0f));
@@ -76,7 +87,7 @@ int main(int argc, char** argv) {
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
 
-    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; bool tail = false; };
+    struct V { const char* name; void (*k)(bsr::GemmArgs); int threads; std::vector<float> t; bool sm = false; bool tail = false; bool nb = false; };
     using namespace bsrlab;
     std::vector<V> vs = {
         {"qs16 + tail (product)", bsr::k_filter_qs16<true, 12>, 512, {}, false, true},
@@ -85,6 +96,9 @@ int main(int argc, char** argv) {
     // timing-only ablations (outputs not compared)
     std::vector<V> abl = {
         {"x sdma no-epi", k_qs16x<kStaticDma | kNoEpi>, 512, {}},
+        {"product, rows |q|<=63", bsr::k_filter_qs16<true, 12>, 512, {}, true, true},
+        {"product, rows+queries |q|<=63", bsr::k_filter_qs16<true, 12>, 512, {}, true, true, true},
+        {"product, queries |q|<=63", bsr::k_filter_qs16<true, 12>, 512, {}, false, true, true},
     };
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
@@ -96,6 +110,7 @@ int main(int argc, char** argv) {
         CHECK(hipMemset(prog, 0, 4096 * 4));
         bsr::GemmArgs gv = g;
         if (v.sm) gv.A = A8s;
+        if (v.nb) gv.B = B8n;
         if (v.tail) gv.tail = cnt + qpad;
         CHECK(hipEventRecord(e0));
         hipLaunchKernelGGL(v.k, dim3(grid), dim3(v.threads), 0, 0, gv);
