@@ -23,7 +23,10 @@ import socket
 import statistics
 import subprocess
 import sys
+import tempfile
+import threading
 import time
+from datetime import timedelta
 
 import numpy as np
 
@@ -72,36 +75,128 @@ def parse():
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] side measurement (N=1)")
     ap.add_argument("--verify", type=int, default=4, help="queries checked against the oracle on rank 0")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="N > 1 without torchrun: the whole run's deadline for the rank processes")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="N > 1: deadline of each collective phase (setup, the step loops, barriers); a "
+                         "rank past it exits non-zero instead of blocking in a collective")
     a = ap.parse_args()
     rows, q, k, dt, sc, label = CONFIGS[a.config]
     a.rows_total = a.rows if a.rows is not None else rows
     a.queries = a.queries if a.queries is not None else q
     a.k = a.k if a.k is not None else k
     a.corpus_dtype, a.scaling, a.label = dt, sc, label
-    # The MFMA candidate filter runs on int8 operands: the bf16 operand (BSR_FLAG_FILTER_BF16,
-    # still a tested library option) is not benchmarked -- DESIGN.md §5.
-    a.filter = "i8"
+    a.filter = "i8"  # the MFMA candidate filter's operand (the bf16 operand is retired)
     if a.config == "c4":
         a.p50_iters = max(a.p50_iters, 100)
     return a
 
 
-def spawn_ranks(n):
-    """Start the N rank processes (one per GPU) and wait; nothing here touches the GPU."""
+def _error_line(args, msg, **extra):
+    """The run's one JSON line when it fails: the metric named, no value."""
+    out = {"metric": "queries/sec + p50 latency, 768-d top-10 over N vectors @1/2/4/8 GPU", "value": None,
+           "unit": "queries/s", "n_gpus": args.gpus, "error": msg}
+    out.update(extra)
+    print(json.dumps(out), flush=True)
+
+
+def spawn_ranks(args):
+    """Start the N rank processes (one per GPU; nothing here touches the GPU) and watch them.
+    Fail fast (metrics.rs:185-197: no rank may be left blocked): the first rank that exits
+    non-zero -- or the run's deadline -- ends every other rank (rank 0 may be blocked in a
+    collective with the dead one), and one JSON error line names the rank and its stderr tail."""
+    n = args.gpus
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = []
+    logdir = tempfile.mkdtemp(prefix="bsr_bench_")
+    procs, errs = [], []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = rc or c
-    return rc
+        ef = open(os.path.join(logdir, f"rank{r}.stderr"), "w+b")
+        errs.append(ef)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stderr=ef))
+    t_end = time.monotonic() + args.rank_timeout
+    failed = None
+    while failed is None:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad[0]
+        elif all(c == 0 for c in codes):
+            break
+        elif time.monotonic() > t_end:
+            failed = (next(r for r, c in enumerate(codes) if c is None), "timeout")
+        else:
+            time.sleep(0.1)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_kill = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    tails = []
+    for r, ef in enumerate(errs):
+        ef.seek(0)
+        data = ef.read().decode(errors="replace")
+        ef.close()
+        sys.stderr.write(data)
+        tails.append(data[-1500:])
+    sys.stderr.flush()
+    if failed is None:
+        return 0
+    r, c = failed
+    what = f"rank {r} exited with status {c}" if c != "timeout" else \
+        f"rank {r} still running after --rank-timeout {args.rank_timeout:.0f} s"
+    _error_line(args, what + "; the other ranks were terminated", failed_rank=r, stderr_tail=tails[r])
+    return c if isinstance(c, int) and c > 0 else 1
+
+
+class Watchdog:
+    """A rank's collective deadline: a phase that has not finished within its time (a peer died
+    inside a collective, a hung transport) ends the process with status 124 and a message,
+    instead of blocking forever (the launcher then ends the other ranks)."""
+
+    def __init__(self, rank):
+        self.rank, self.deadline, self.label = rank, None, ""
+        self.lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def arm(self, label, seconds):
+        with self.lock:
+            self.label, self.deadline = label, time.monotonic() + seconds
+
+    def disarm(self):
+        with self.lock:
+            self.deadline = None
+
+    def save(self):
+        with self.lock:
+            return self.label, self.deadline
+
+    def restore(self, state):
+        with self.lock:
+            self.label, self.deadline = state
+
+    def _run(self):
+        while True:
+            time.sleep(0.5)
+            with self.lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                label = self.label
+            if late:
+                sys.stderr.write(f"bench.py rank {self.rank}: collective phase '{label}' passed its deadline "
+                                 f"(--collective-timeout); exiting\n")
+                sys.stderr.flush()
+                os._exit(124)
 
 
 def cpu_model():
@@ -230,17 +325,24 @@ def main():
         sys.exit(run_c1(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
 
+    # (test hook of the fail-fast path: this rank fails before its first collective)
+    if os.environ.get("BSR_BENCH_FAIL_RANK") == str(rank) and world > 1:
+        sys.stderr.write(f"bench.py rank {rank}: failing on purpose (BSR_BENCH_FAIL_RANK)\n")
+        sys.exit(3)
+
     import torch
     import bsr
 
+    wd = Watchdog(rank) if world > 1 else None
     dist = None
     if world > 1:
+        wd.arm("process group init", args.collective_timeout)
         import torch.distributed as dist
         # (gloo prints its connection report to stdout: keep stdout for the one JSON line)
         sys.stdout.flush()
@@ -251,15 +353,26 @@ def main():
         finally:
             os.dup2(saved_fd, 1)
             os.close(saved_fd)
+        wd.disarm()
     ndev = torch.cuda.device_count()
     device = local_rank % max(ndev, 1)
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
 
-    def barrier():
+    def barrier(timeout=None):
+        """Every rank here, or a named failure: gloo's monitored barrier reports the rank that
+        did not arrive (the bootstrap group is gloo), under the collective deadline."""
         torch.cuda.synchronize()
         if dist:
-            dist.barrier()
+            t = timeout or args.collective_timeout
+            prev = wd.save()
+            wd.arm("barrier", t + 30)
+            dist.monitored_barrier(timeout=timedelta(seconds=t))
+            wd.restore(prev)
+
+    def armed(label):
+        if wd:
+            wd.arm(label, args.collective_timeout)
 
     D, Q, K = args.dim, args.queries, args.k
     n_total = args.rows_total * (world if args.scaling == "weak" else 1)
@@ -296,6 +409,7 @@ def main():
     torch.cuda.synchronize()
 
     comm = None
+    armed("communicator setup")
     if world > 1:
         if args.comm == "host":
             comm = bsr.Comm.host(dist.group.WORLD)
@@ -325,6 +439,7 @@ def main():
 
     # Clock settle: the same number of untimed searches on every rank (each search is a
     # collective for N > 1), sized on rank 0 from one search's time.
+    armed("settle + warmup steps")
     step()
     t1 = time.perf_counter()
     step()
@@ -340,6 +455,7 @@ def main():
     index.profile(reset=True)
     stats_fb = stats_rescued = 0
     barrier()
+    armed("timed steps")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -348,6 +464,7 @@ def main():
         stats_rescued += ls.n_rescued
     barrier()
     elapsed = time.perf_counter() - t0
+    armed("stage-profile, local-search and p50 passes")
     prof = index.profile(reset=True)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -602,7 +719,9 @@ def main():
     if rank == 0:
         out.setdefault("cpu_baseline", None)  # N > 1: the baseline is measured at N = 1 only
         print(json.dumps(out), flush=True)
-    barrier()
+    if wd:
+        wd.disarm()
+    barrier(timeout=max(args.collective_timeout, 1200))  # (rank 0's spot-check and CPU sweep ran)
     if comm:
         comm.close()
     index.close()

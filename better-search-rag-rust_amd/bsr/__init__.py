@@ -46,8 +46,8 @@ BSR_BF16 = 1
 BSR_MAX_K = 256
 BSR_FLAG_EXACT_ONLY = 1
 BSR_FLAG_PROFILE = 2
-BSR_FLAG_FILTER_BF16 = 4
-FILTER_I8, FILTER_BF16 = 0, 1
+BSR_FLAG_FILTER_BF16 = 4   # retired (round 4): bsr_index_create returns BSR_E_INVALID
+FILTER_I8 = 0
 ROOT = 0  # src/mpi_helpers/mod.rs:8
 
 
@@ -508,29 +508,36 @@ def gather_global_top_k(world, local_idx, local_dist, local_count, top_k: int):
     src/mpi_helpers/metrics.rs:194-202) for a batch: local lists [Q, top_k] (+ counts [Q]) of
     this rank, or all None for an empty contribution.  Root: (idx, dist, count) of the
     global top-k; other ranks: None.  `world` None (one rank): the local lists merged alone."""
-    if local_idx is None:
-        q = None
-    else:
+    q, err = None, None
+    if local_idx is not None:
         local_idx = np.ascontiguousarray(local_idx, np.uint64)
         local_dist = np.ascontiguousarray(local_dist, np.float32)
         local_count = np.ascontiguousarray(local_count, np.uint32)
-        q = local_idx.shape[0]
+        q = local_idx.shape[0] if local_idx.ndim else 0
         # the library reads Q * top_k entries of each list and Q counts
         if local_idx.shape != (q, top_k) or local_dist.shape != (q, top_k) or local_count.shape != (q,):
-            raise BsrError(-1, f"local lists must be [Q, top_k] = [{q}, {top_k}] (+ counts [Q]); got "
-                               f"{local_idx.shape}, {local_dist.shape}, {local_count.shape}")
+            err = (f"local lists must be [Q, top_k] = [{q}, {top_k}] (+ counts [Q]); got "
+                   f"{local_idx.shape}, {local_dist.shape}, {local_count.shape}")
     comm = _as_comm(world)
     if comm is None:
+        if err:
+            raise BsrError(-1, err)
         if q is None:
             raise BsrError(-1, "one rank (world=None) with no local lists: nothing to merge")
         return merge_top_k_lists(local_idx[None], local_dist[None], local_count[None], top_k)
-    nq = q if q is not None else 0
-    # every rank must agree on the batch size: take it from the ranks that have lists
-    nq = int(max(np.frombuffer(b"".join(comm.allgather_bytes(np.uint32(nq).tobytes())), np.uint32)))
-    if q is not None and q != nq:
-        # a mismatched list exchange is undefined: take part with an empty list, then fail
-        _ = lib().bsr_gather_global_top_k(comm._h, None, None, None, nq, top_k, None, None, None)
-        raise BsrError(-1, f"this rank has {q} queries, another has {nq}")
+    # Every rank's {has lists, Q, top_k, valid} first, and every check after it: a rank that
+    # raised before the exchange would leave the others blocked in it, and ranks that disagree
+    # on the batch shape must all fail before any list moves (as the C parallel search does).
+    mine = np.array([q is not None, q or 0, top_k, err is not None], np.uint32)
+    hdr = np.frombuffer(b"".join(comm.allgather_bytes(mine.tobytes())), np.uint32).reshape(comm.size, 4)
+    bad = [r for r in range(comm.size) if hdr[r, 3]]
+    if bad:
+        raise BsrError(-1, err if err else f"rank(s) {bad} passed invalid local lists; no rank exchanged lists")
+    shapes = {int(hdr[r, 1]) for r in range(comm.size) if hdr[r, 0]}
+    if len(shapes) > 1 or len({int(x) for x in hdr[:, 2]}) > 1:
+        raise BsrError(-1, f"ranks disagree on the batch shape (Q per rank {hdr[:, 1].tolist()}, top_k per rank "
+                           f"{hdr[:, 2].tolist()}); no rank exchanged lists")
+    nq = shapes.pop() if shapes else 0
     oi = np.empty((nq, top_k), np.uint64)
     od = np.empty((nq, top_k), np.float32)
     oc = np.empty(nq, np.uint32)
@@ -577,8 +584,16 @@ def parallel_top_k_similarity_search_batch(world, index: Optional[Index], querie
         rank = comm.rank if comm is not None else ROOT
     if isinstance(queries, np.ndarray) or not hasattr(queries, "data_ptr"):
         queries = np.ascontiguousarray(queries, np.float32)
-        if queries.ndim == 1:
-            queries = queries.reshape(1, -1)
+    if queries.ndim == 1:
+        queries = queries.reshape(1, -1)
+    if queries.ndim != 2:
+        raise BsrError(-1, f"queries must be [Q, dim]; got shape {tuple(queries.shape)}")
+    if not isinstance(queries, np.ndarray):
+        import torch
+        if queries.dtype != torch.float32 or not queries.is_contiguous():
+            raise BsrError(-1, "query tensors must be contiguous float32")
+    if index is not None and int(queries.shape[1]) != index.dim:
+        raise BsrError(-6, f"query length {int(queries.shape[1])} != dim {index.dim}")
     nq = int(queries.shape[0])
     oi = np.empty((nq, top_k), np.uint64)
     od = np.empty((nq, top_k), np.float32)

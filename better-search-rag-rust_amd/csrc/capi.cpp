@@ -96,6 +96,7 @@ struct bsr_comm {
     PinnedVec<uint32_t> h_nan;
     DevBuf hdr_send, hdr_recv;     // the parallel search's shape agreement (RCCL)
     PinnedVec<int32_t> h_hdr;      // [1 + size][kHdrWords]: this rank's words, then every rank's
+    bool hdr_posted = false;       // this search's header all-gather has been issued
 };
 
 // The parallel search's header, all-gathered before the lists: every rank's batch shape
@@ -541,8 +542,19 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
 // c->h_hdr[1 + r]: through the host transport (synchronous), or as a 16-byte RCCL all-gather
 // on c->stream that header_wait() completes -- enqueued before the local search, so its
 // latency hides behind the search.
-static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
+// Fault injection for the collective-safety tests (BSR_INJECT_FAULT=header_hook[:rank]): the
+// header all-gather issued from the search's hook fails before it is posted, as a buffer that
+// cannot be sized would make it fail.
+static bool inject_header_hook_fault(const bsr_comm* c) {
+    static const char* v = getenv("BSR_INJECT_FAULT");
+    if (!v || strncmp(v, "header_hook", 11) != 0) return false;
+    return v[11] != ':' || atoi(v + 12) == c->rank;
+}
+
+static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool from_hook = false) {
     const size_t P = (size_t)c->size, hb = kHdrWords * sizeof(int32_t);
+    if (from_hook && inject_header_hook_fault(c))
+        return set_error(BSR_E_NOMEM, "injected fault: header buffers (BSR_INJECT_FAULT)");
     BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));
     int32_t* h = c->h_hdr.data();
     h[0] = (int32_t)nq;
@@ -550,6 +562,7 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
     h[2] = st;
     h[3] = kHdrMagic;
     if (c->host_fn) {
+        c->hdr_posted = true;  // (a failing transport fails on every rank)
         if (c->host_fn(h, h + kHdrWords, hb, c->host_user) != 0)
             return set_error(BSR_E_RCCL, "host all-gather callback failed");
         return BSR_OK;
@@ -559,6 +572,7 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st) {
     BSR_TRY(c->hdr_recv.ensure(hb * P));
     BSR_HIP(hipMemcpyAsync(c->hdr_send.p, h, hb, hipMemcpyHostToDevice, c->stream));
     BSR_NCCL(ncclAllGather(c->hdr_send.p, c->hdr_recv.p, hb, ncclUint8, c->comm, c->stream));
+    c->hdr_posted = true;
     BSR_HIP(hipMemcpyAsync(h + kHdrWords, c->hdr_recv.p, hb * P, hipMemcpyDeviceToHost, c->stream));
     return BSR_OK;
 }
@@ -595,17 +609,19 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     struct HookCtx { bsr_comm* c; uint32_t nq, k; int32_t st; } hc{c, nq, k, st};
     auto hook = [](void* p) -> int {
         const HookCtx* h = static_cast<const HookCtx*>(p);
-        return header_start(h->c, h->nq, h->k, h->st);
+        return header_start(h->c, h->nq, h->k, h->st, true);
     };
-    bool header_issued = false;
+    if (c) c->hdr_posted = false;
     // compute_local_top_k (:185-191)
     if (st == BSR_OK) {
         st = ix->search_device(queries, nq, k, multi ? +hook : nullptr, &hc);
-        header_issued = multi && ix->launched_hook;
         // (a failed header all-gather is a transport error: every rank sees it; report it)
-        if (header_issued && st == BSR_E_RCCL) return st;
+        if (multi && c->hdr_posted && st == BSR_E_RCCL) return st;
     }
-    if (multi && !header_issued) BSR_TRY(header_start(c, nq, k, st));
+    // The header collective must be posted exactly once whatever failed before it (the search,
+    // or the hook itself before its all-gather: a buffer it could not size): then it carries
+    // this rank's error status, so the peers are never left in a collective this rank skipped.
+    if (multi && !c->hdr_posted) BSR_TRY(header_start(c, nq, k, st));
     if (!c) {  // one rank, no communicator: the local lists are the result
         BSR_TRY(st);
         if (!nq) return BSR_OK;

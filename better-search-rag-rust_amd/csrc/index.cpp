@@ -2,14 +2,14 @@
 // (compute_local_top_k, src/mpi_helpers/metrics.rs:16-53, for a batch of queries).
 //
 // Pipeline for a batch, all on the index's stream:
-//   1. query prep     exact |b| (src/metrics.rs:155), flags, the filter operand (int8 + scale,
-//                     or bf16) and the per-query certification bound E_q
+//   1. query prep     exact |b| (src/metrics.rs:155), flags, the filter operand (int8 + scale)
+//                     and the per-query certification bound E_q
 //   2. sample filter  MFMA scores of every 32nd row -> tau0 (per query)
 //   3. emit filter    MFMA scores of every row; rows with score >= tau0 -> candidates
 //   4. select         top-(k'+1) candidates by approximate score
 //   5. rescore        exact sequential-f32 distances of k' candidates, top-k, certify
 //   6. one status readback; fallback: exact full scan of any uncertified / ineligible query
-// Small batches, k > 200, or an index with out-of-range norms use the exact scan only.
+// k > 200, or an index with out-of-range norms, use the exact scan only.
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -21,7 +21,6 @@
 
 namespace bsr {
 
-constexpr uint32_t kMinBatchForFilter = 16;
 constexpr uint32_t kMaxKForFilter = 200;
 
 static thread_local std::string g_err;
@@ -176,6 +175,10 @@ static int index_prepare_rows(bsr_index* ix, const void* rows, uint64_t n_rows, 
     const bool dev = is_device_ptr(rows);
     const size_t elem = ix->cfg.dtype == BSR_BF16 ? 2 : 4;
     const void* src = rows;
+    // Device rows may still be in flight on ANY stream of the caller (a torch side stream, a
+    // communication stream): the ABI has no stream argument, and a load runs once, outside
+    // any timed region, so a full device synchronize costs nothing and removes the hazard.
+    if (dev) BSR_HIP(hipDeviceSynchronize());
     if (!dev) {
         BSR_TRY(ix->tmp.ensure(n_rows * (size_t)ix->dim * elem));
         BSR_HIP(hipMemcpyAsync(ix->tmp.p, rows, n_rows * (size_t)ix->dim * elem, hipMemcpyHostToDevice,
@@ -198,30 +201,18 @@ static int index_finish_load(bsr_index* ix) {
     BSR_HIP(hipMemsetAsync(ix->na.p, 0, ix->n_pad * sizeof(float), ix->stream));
     if (ix->n) BSR_HIP(launch_row_norms(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->na.as<float>(),
                                         ix->flags.as<uint32_t>(), ix->stream));
-    if (ix->op == kFilterBF16) {
-        BSR_HIP(launch_rows_to_bf16n(ix->rows.as<float>(), ix->na.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld,
-                                     ix->fop.as<uint16_t>(), ix->stream));
-    } else {
-        BSR_TRY(ix->ascale.ensure(ix->n_pad / kQuantBlock * sizeof(float)));
-        BSR_HIP(launch_rows_to_i8(ix->rows.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld, ix->fop.as<int8_t>(),
-                                  ix->ascale.as<float>(), ix->flags.as<uint32_t>() + 1, ix->stream));
-    }
+    BSR_TRY(ix->ascale.ensure(ix->n_pad / kQuantBlock * sizeof(float)));
+    BSR_HIP(launch_rows_to_i8(ix->rows.as<float>(), ix->n, ix->n_pad, ix->dim, ix->ld, ix->fop.as<int8_t>(),
+                              ix->ascale.as<float>(), ix->flags.as<uint32_t>() + 1, ix->stream));
     // The sample pass reads every kSampleStride-th row: those rows, contiguous (1/32 of the
-    // operand bytes), so that it streams whole rows; int8 indexes quantize them with one scale
-    // per filter tile of sampled rows (its epilogue then takes integer maxima).
+    // operand bytes), so that it streams whole rows, quantized with one scale per filter tile
+    // of sampled rows (its epilogue then takes integer maxima).
     const uint64_t n_s = (ix->n + kSampleStride - 1) / kSampleStride;
     const uint64_t n_s_pad = round_up(std::max<uint64_t>(n_s, 1), kSampleScaleRows);
     BSR_TRY(ix->fop_s.ensure((size_t)n_s_pad * ix->op_row_bytes));
-    if (ix->op == kFilterBF16) {
-        if (n_s)
-            BSR_HIP(hipMemcpy2DAsync(ix->fop_s.p, ix->op_row_bytes, ix->fop.p,
-                                     (size_t)ix->op_row_bytes * kSampleStride, ix->op_row_bytes, n_s,
-                                     hipMemcpyDeviceToDevice, ix->stream));
-    } else {
-        BSR_TRY(ix->ascale_s.ensure((size_t)(n_s_pad / kSampleScaleRows) * sizeof(float)));
-        BSR_HIP(launch_rows_to_i8_sample(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->fop_s.as<int8_t>(),
-                                         ix->ascale_s.as<float>(), ix->stream));
-    }
+    BSR_TRY(ix->ascale_s.ensure((size_t)(n_s_pad / kSampleScaleRows) * sizeof(float)));
+    BSR_HIP(launch_rows_to_i8_sample(ix->rows.as<float>(), ix->n, ix->dim, ix->ld, ix->fop_s.as<int8_t>(),
+                                     ix->ascale_s.as<float>(), ix->stream));
     uint32_t f[2] = {0, 0};
     BSR_HIP(hipMemcpyAsync(f, ix->flags.p, sizeof f, hipMemcpyDeviceToHost, ix->stream));
     BSR_HIP(hipStreamSynchronize(ix->stream));
@@ -242,6 +233,11 @@ int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
     *out = nullptr;
     if (cfg->dim == 0) return set_error(BSR_E_INVALID, "dim must be >= 1");
     if (cfg->dtype != BSR_F32 && cfg->dtype != BSR_BF16) return set_error(BSR_E_INVALID, "unknown dtype");
+    // The bf16 filter operand (rounds 1-3) is retired: the int8 operand runs at twice the MFMA
+    // rate with an equally tight certification bound; a bf16 CORPUS (dtype)
+    // is still served, on the int8 filter.
+    if (cfg->flags & BSR_FLAG_FILTER_BF16)
+        return set_error(BSR_E_INVALID, "BSR_FLAG_FILTER_BF16 is retired (the filter operand is int8)");
     if (cfg->max_k == 0 || cfg->max_k > BSR_MAX_K)
         return set_error(BSR_E_INVALID, "max_k must be in [1, %u]", BSR_MAX_K);
     BSR_TRY(select_device(cfg->device));
@@ -253,8 +249,7 @@ int bsr_index_create_impl(const bsr_config* cfg, bsr_index** out) {
     ix->device = dev;
     ix->dim = cfg->dim;
     ix->ld = (uint32_t)round_up(cfg->dim, kLdAlign);
-    ix->op = (cfg->flags & BSR_FLAG_FILTER_BF16) ? kFilterBF16 : kFilterI8;
-    ix->op_row_bytes = ix->op == kFilterBF16 ? ix->ld * 2 : ix->ld;
+    ix->op_row_bytes = ix->ld;  // int8 filter operand rows
     // A blocking stream: its work waits for work issued earlier on the legacy default (NULL)
     // stream -- PyTorch's default stream -- so device rows or queries a caller has just
     // produced there are complete before the library reads them (the ABI has no stream
@@ -387,7 +382,7 @@ static uint32_t cap_for(uint32_t k) { return 16u * (kp_for(k) + 1u); }
 // Candidate stage (steps 2-5) for every query of the batch.  Batches of at most 16
 // queries on an int8 index use the skinny (HBM-bound, no LDS) filter kernels.
 static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint32_t* next_status) {
-    const bool skinny = ix->op == kFilterI8 && nq <= kSkinnyMaxQ;
+    const bool skinny = nq <= kSkinnyMaxQ;
     // k' candidates, (k'+1) % 64 == 0, about 3k: the k-th exact score must clear the (k'+1)-th
     // approximate one by E_q, and in a Gaussian-like tail that takes ~3x as many rows at
     // E_q/sigma ~ 0.26.  63 for k <= 10, 191 for k = 50, 383 for k = 100.
@@ -439,7 +434,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
         g.s_compact = compact ? 1u : 0u;
         BSR_HIP(launch_timed(ix, ix->ev_sample, [&](hipEvent_t e0, hipEvent_t e1) {
             return skinny ? launch_filter_skinny_sample(g, ix->stream, e0, e1)
-                          : launch_filter_sample(ix->op, g, ix->stream, e0, e1);
+                          : launch_filter_sample(g, ix->stream, e0, e1);
         }, 2));
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
                                   ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
@@ -462,7 +457,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     g.tail = g.n_qt <= kTailCounters ? ix->cnt.as<uint32_t>() + qpad : nullptr;
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return skinny ? launch_filter_skinny_emit(g, ix->stream, e0, e1)
-                      : launch_filter_emit(ix->op, g, ix->stream, e0, e1);
+                      : launch_filter_emit(g, ix->stream, e0, e1);
     }));
     // lists of <= 1024 keys (k <= 10): the rescore kernel selects its own k' candidates
     const bool fused_select = cap <= kFusedSelectCap;
@@ -535,13 +530,12 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
 int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*),
                              void* ctx) {
     bsr_index* ix = this;
-    launched_hook = false;
     if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
     if (k == 0 || k > ix->cfg.max_k) return set_error(BSR_E_INVALID, "k=%u outside [1, max_k=%u]", k, ix->cfg.max_k);
     BSR_HIP(hipSetDevice(ix->device));
     stats = bsr_search_stats{};
     stats.n_queries = nq;
-    stats.filter_op = (uint32_t)op;
+    stats.filter_op = 0;  // int8
     stats.row_ebound = row_ebound;
     // packed result layout for this batch
     const size_t nqk = (size_t)std::max(nq, 1u) * k;
@@ -594,17 +588,14 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
         qsrc = q_in.as<float>();
     }
     // (the status words of res[cur] were zeroed by the previous search's finalize)
-    // int8 indexes filter every batch (small ones with the skinny kernels); bf16 indexes
-    // only batches of >= 16 queries (smaller ones take the exact scan).
-    const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter &&
-                            (op == kFilterI8 || nq >= kMinBatchForFilter);
+    // every batch is filtered (batches of <= 16 queries by the skinny kernels)
+    const bool use_filter = n > 0 && approx_ok && k <= kMaxKForFilter;
     QueryPrepArgs qa{};
     qa.q = qsrc;
     qa.nq = nq;
     qa.qpad = qpad;
     qa.dim = dim;
     qa.ld = ld;
-    qa.op = op;
     qa.ea_max = flags.as<uint32_t>() + 1;
     qa.qf32 = qf32.as<float>();
     qa.nb = nb.as<float>();
@@ -683,10 +674,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     }
     next_status_clean = true;
     int hook_st = BSR_OK;
-    if (after_launch) {
-        launched_hook = true;
-        hook_st = after_launch(ctx);
-    }
+    if (after_launch) hook_st = after_launch(ctx);
     BSR_HIP(stream_wait(stream));
     if (hook_st != BSR_OK) return hook_st;
     // Later rounds (second-chance rescore, scan) finalize and read back again, directly.

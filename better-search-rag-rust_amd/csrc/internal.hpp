@@ -70,13 +70,12 @@ struct bsr_index {
     bool loaded = false;
     bool approx_ok = false;
     uint32_t row_flags = 0;
-    bsr::FilterOp op = bsr::kFilterI8;  // MFMA filter operand type (BSR_FLAG_FILTER_BF16)
     uint32_t op_row_bytes = 0;          // bytes of one filter operand row
     float row_ebound = 0.0f;            // int8: max_row ||a/|a| - s q||_2 (certification)
 
     bsr::DevBuf rows;   // f32 [n_pad][ld], zero padded: the reference's values
     bsr::DevBuf na;     // f32 [n_pad]: exact magnitudes (src/metrics.rs:154)
-    bsr::DevBuf fop;    // filter operand rows: int8 or bf16 [n_pad][ld]
+    bsr::DevBuf fop;    // filter operand rows: int8 [n_pad][ld]
     bsr::DevBuf fop_s;  // every kSampleStride-th row as the sample pass's operand, contiguous
     bsr::DevBuf ascale_s; // int8: f32 [n_s_pad / kSampleScaleRows] sample operand scales
     bsr::DevBuf ascale; // int8: f32 [n_pad/32] block scales
@@ -130,5 +129,4 @@ struct bsr_index {
     // its shape-agreement collective there); its non-OK status is returned after the wait.
     int search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*) = nullptr,
                       void* ctx = nullptr);
-    bool launched_hook = false;  // after_launch ran during the last search_device
 };

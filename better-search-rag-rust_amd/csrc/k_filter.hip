@@ -5,13 +5,11 @@
 // distance: the candidates are rescored with the reference's exact arithmetic
 // (k_exact.hip) and the final list is certified against the filter's error bound.
 //
-// Two operand types share one kernel (template Op):
-//   OpI8   int8 rows (per 32-row block scale) x int8 queries (per query scale) on
-//          v_mfma_i32_32x32x32_i8; the integer dot product is exact, the score is
-//          ((float)I * s_row_block) * s_query.
-//   OpBF16 bf16(a/|a|) x bf16(b/|b|) on v_mfma_f32_32x32x16_bf16.
-// Both move 64 bytes of K per row per slice, so the tiling, the LDS ring and the issue
-// schedule are identical; an int8 slice carries twice the K of a bf16 slice.
+// Operands: int8 rows (per 32-row block scale) x int8 queries (per query scale); the integer
+// dot product is exact, the score is ((float)I * s_row_block) * s_query.  The product kernel
+// is k_filter_qs16 (v_mfma_i32_16x16x64_i8, rows of an even number of 64-byte K slices up to
+// 768 bytes); k_filter (v_mfma_i32_32x32x32_i8) serves the other row widths.  (The bf16
+// operand of rounds 1-3 is retired: half the int8 MFMA rate at an equal bound.)
 #include "bsr_device.hpp"
 #include "kernels.hpp"
 
@@ -24,20 +22,10 @@
 
 namespace bsr {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 typedef __attribute__((ext_vector_type(16))) int i32x16_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-struct OpBF16 {
-    using frag_t = bf16x8_t;
-    using acc_t = f32x16_t;
-    static constexpr bool kInt = false;
-    __device__ __forceinline__ static acc_t mfma(const frag_t& a, const frag_t& b, const acc_t& c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-    }
-};
 struct OpI8 {
     using frag_t = i32x4_t;
     using acc_t = i32x16_t;
@@ -1303,12 +1291,12 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 }
 
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the query-stationary
-// kernel; other int8 widths and the bf16 operand: k_filter.  (A one-wave-per-SIMD variant
+// kernel; other widths: k_filter.  (A one-wave-per-SIMD variant
 // with 64 queries per wave, tools/microbench/k_qs64_lab.hip, measured slower: DESIGN.md §5.)
 template <bool EMIT>
-static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_filter(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
-    if (op == kFilterI8 && nk % 2 == 0 && nk <= 12) {
+    if (nk % 2 == 0 && nk <= 12) {
         const dim3 g(grid), b(512);
         switch (nk) {
             case 2: BSR_KLAUNCH((k_filter_qs16<EMIT, 2>), g, b, s, e0, e1, a); return;
@@ -1319,17 +1307,14 @@ static void launch_filter(FilterOp op, const GemmArgs& a, hipStream_t s, hipEven
             default: BSR_KLAUNCH((k_filter_qs16<EMIT, 12>), g, b, s, e0, e1, a); return;
         }
     }
-    if (op == kFilterI8)
-        BSR_KLAUNCH((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
-    else
-        BSR_KLAUNCH((k_filter<OpBF16, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
+    BSR_KLAUNCH((k_filter<OpI8, EMIT>), dim3(grid), dim3(kThreads), s, e0, e1, a);
 }
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_filter<false>(op, a, s, e0, e1);
+hipError_t launch_filter_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_filter<false>(a, s, e0, e1);
     return hipGetLastError();
 }
-hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_filter<true>(op, a, s, e0, e1);
+hipError_t launch_filter_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    launch_filter<true>(a, s, e0, e1);
     return hipGetLastError();
 }
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,

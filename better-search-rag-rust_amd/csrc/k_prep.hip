@@ -1,5 +1,5 @@
 // k_prep.hip -- data movement and preparation kernels (gfx950): synthetic data, the padded
-// f32 slab, the reference's exact magnitudes, and the MFMA filter operands (bf16 or int8)
+// f32 slab, the reference's exact magnitudes, and the MFMA filter operands (int8)
 // of corpus rows and queries together with their certification error bounds.
 //
 // Compiled with -ffp-contract=off: the magnitudes reproduce src/metrics.rs:154-155 (a
@@ -108,33 +108,6 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ row
     }
     const uint32_t any = __reduce_or_sync(~0ull, f);
     if (any && lane_id() == 0) atomicOr(flags, any);
-}
-
-// Normalised bf16 copy for the bf16 filter: bf16_rne(a_i / |a|), zero rows / pad -> 0.
-// Each thread writes 8 consecutive elements (16 B).
-__global__ void k_rows_to_bf16n(const float* __restrict__ rows, const float* __restrict__ na,
-                                uint64_t n, uint64_t n_pad, uint32_t dim, uint32_t ld,
-                                uint16_t* __restrict__ out) {
-    const uint64_t groups = n_pad * (uint64_t)(ld / 8);
-    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < groups;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t r = g / (ld / 8);
-        const uint32_t c0 = (uint32_t)(g - r * (ld / 8)) * 8;
-        uint16_t h[8];
-        const float m = r < n ? na[r] : 0.0f;
-        const bool ok = r < n && m != 0.0f && isfinite(m);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t c = c0 + j;
-            h[j] = (ok && c < dim) ? f32_to_bf16_rne(rows[r * ld + c] / m) : (uint16_t)0;
-        }
-        uint4 v;
-        v.x = h[0] | ((uint32_t)h[1] << 16);
-        v.y = h[2] | ((uint32_t)h[3] << 16);
-        v.z = h[4] | ((uint32_t)h[5] << 16);
-        v.w = h[6] | ((uint32_t)h[7] << 16);
-        *reinterpret_cast<uint4*>(out + r * ld + c0) = v;
-    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -301,12 +274,10 @@ __global__ __launch_bounds__(256) void k_rows_to_i8_sample(const float* __restri
 //   2. wave 0's lane 0 walks the row in index order: |b| exactly as src/metrics.rs:155 (sequential
 //      f32 sum of squares from -0.0, correctly rounded sqrt), finiteness
 //   3. flags, the identity query-id list of the exact scan (min(q, nq-1))
-//   4. the filter operand from the LDS copy:
-//        bf16: bf16_rne(b_i / |b|), E_q = the constant bf16 bound
-//        int8: x = b/|b| (double), s = smallest f32 >= max|x_i|/127, q_i = rint(x_i/s),
-//              eb = ||x - s q||_2, E_q = ea + eb + ea*eb + 1.5e-4 (ea: the row side; 1.5e-4
-//              covers the reference's own f32 rounding, <= 9.3e-5, and the two f32 roundings
-//              of the filter's score)
+//   4. the int8 filter operand from the LDS copy: x = b/|b| (double), s = smallest f32 >=
+//      max|x_i|/127, q_i = rint(x_i/s), eb = ||x - s q||_2, E_q = ea + eb + ea*eb + 1.5e-4 (ea:
+//      the row side; 1.5e-4 covers the reference's own f32 rounding, <= 9.3e-5, and the two f32
+//      roundings of the filter's score)
 //      queries the filter cannot serve (pad, zero/tiny/huge |b|) get a zero operand and
 //      E_q = inf.
 // ------------------------------------------------------------------------------------
@@ -316,14 +287,13 @@ constexpr uint32_t kQueryLdsFloats = 8192;  // rows up to 8192 floats are staged
 // dependent chain of f32 adds), wave 1 quantises the row to int8 (double precision) into
 // registers; the result is kept only if |b| admits the filter (else zeros, E_q = inf).
 __global__ __launch_bounds__(128) void k_query_prep(const float* __restrict__ q, uint32_t nq, uint32_t dim,
-                                                    uint32_t ld, FilterOp op, bool with_op,
+                                                    uint32_t ld, bool with_op,
                                                     const uint32_t* __restrict__ ea_max,
                                                     float* __restrict__ qf32, float* __restrict__ nb,
                                                     void* __restrict__ qop, float* __restrict__ qscale,
                                                     float* __restrict__ ebound, uint32_t* __restrict__ qflags,
                                                     int32_t* __restrict__ qids, uint32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) float row[kQueryLdsFloats];
-    __shared__ float s_mag;
     __shared__ uint32_t s_flags;
     __shared__ uint32_t s_bad;
     const uint32_t qi = blockIdx.x;
@@ -358,7 +328,7 @@ __global__ __launch_bounds__(128) void k_query_prep(const float* __restrict__ q,
     __syncthreads();
     bad = s_bad != 0;
     auto val = [&](uint32_t c) -> float { return staged ? row[c] : dst[c]; };
-    const bool i8 = with_op && op != kFilterBF16;
+    const bool i8 = with_op;
     // wave 1 (int8 operand): the quantisation, speculatively, into registers
     constexpr int QV = 4;  // char4 groups per lane held (rows up to 1024 int8); longer rows: second pass
     char4 qv[QV];
@@ -424,21 +394,11 @@ __global__ __launch_bounds__(128) void k_query_prep(const float* __restrict__ q,
         qflags[qi] = f;
         qids[qi] = (int32_t)(real ? qi : (nq ? nq - 1 : 0));
         if (f & kQueryNonFinite) atomicOr(status + kStQueryFlags, kQueryNonFinite);
-        s_mag = m;
         s_flags = f;
     }
     __syncthreads();
     const bool ok = !(s_flags & kQueryNoApprox);
-    if (!with_op) return;
-    if (op == kFilterBF16) {
-        uint16_t* o = static_cast<uint16_t*>(qop) + (uint64_t)qi * ld;
-        const float m = ok ? s_mag : 1.0f;
-        for (uint32_t c = t; c < ld; c += 128)
-            o[c] = (ok && c < dim) ? f32_to_bf16_rne(val(c) / m) : (uint16_t)0;
-        if (t == 0) ebound[qi] = ok ? (float)kEBoundBF16 : INFINITY;
-        return;
-    }
-    if (w != 1) return;
+    if (!with_op || w != 1) return;
     // wave 1: keep the speculative operand (the filter serves this query) or zero it
     int8_t* o = static_cast<int8_t*>(qop) + (uint64_t)qi * ld;
     for (uint32_t g = 0, c0 = lane * 4; c0 < ld; ++g, c0 += 4 * kWave) {
@@ -488,12 +448,6 @@ hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t dim, uint32_
                        na, flags);
     return hipGetLastError();
 }
-hipError_t launch_rows_to_bf16n(const float* rows, const float* na, uint64_t n, uint64_t n_pad,
-                                uint32_t dim, uint32_t ld, uint16_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_rows_to_bf16n, dim3(grid_for(n_pad * (ld / 8), 256)), dim3(256), 0, s, rows, na, n,
-                       n_pad, dim, ld, out);
-    return hipGetLastError();
-}
 hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint32_t dim, uint32_t ld,
                              int8_t* out, float* scales, uint32_t* ea_max, hipStream_t s) {
     const uint64_t blocks = n_pad / kQuantBlock;
@@ -511,7 +465,7 @@ hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim,
     return hipGetLastError();
 }
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(128), 0, s, a.q, a.nq, a.dim, a.ld, a.op, a.with_op,
+    hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(128), 0, s, a.q, a.nq, a.dim, a.ld, a.with_op,
                        a.ea_max, a.qf32, a.nb, a.qop, a.qscale, a.ebound, a.qflags, a.qids, a.status);
     return hipGetLastError();
 }

@@ -16,12 +16,6 @@ constexpr uint32_t kQuantBlock = 32;   // rows sharing one int8 scale (one 32-ro
 constexpr uint32_t kSampleScaleRows = 128; // int8 sample rows sharing one scale (one filter tile)
 constexpr uint32_t kFilterTile = 256;  // MFMA filter tile: 256 corpus rows x 256 queries
 
-// Operand type of the MFMA candidate filter.
-enum FilterOp : uint32_t {
-    kFilterI8 = 0,    // int8 rows/queries, per-32-row-block and per-query scales, i32 MFMA
-    kFilterBF16 = 1,  // bf16(a/|a|), bf16(b/|b|), f32-accumulating bf16 MFMA
-};
-
 // Row-state flags (index load).
 constexpr uint32_t kRowNonFinite = 1u;  // a NaN/Inf element
 constexpr uint32_t kRowNormOvf = 2u;    // sum of squares overflowed
@@ -34,9 +28,6 @@ constexpr uint32_t kQueryNoApprox = 2u;   // norm zero/tiny/huge: answered by th
 // Search status words (device, one small D2H copy per search).
 enum StatusWord : uint32_t { kStFail = 0, kStEmitted = 1, kStQueryFlags = 2, kStFail2 = 3, kStWords = 4 };
 
-// Certification bound of the bf16 filter.
-constexpr double kEBoundBF16 = 8.5e-3;
-
 // ---- data movement / load-time preparation (k_prep.hip) -------------------------------
 hipError_t launch_synth_uniform(float* out, uint64_t row0, uint64_t n_rows, uint32_t dim,
                                 uint32_t ld, uint64_t seed, hipStream_t s);
@@ -46,8 +37,6 @@ hipError_t launch_widen_bf16_rows(const uint16_t* src, uint64_t n, uint32_t dim,
                                   float* dst, hipStream_t s);
 hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t dim, uint32_t ld,
                             float* na, uint32_t* flags, hipStream_t s);
-hipError_t launch_rows_to_bf16n(const float* rows, const float* na, uint64_t n, uint64_t n_pad,
-                                uint32_t dim, uint32_t ld, uint16_t* out, hipStream_t s);
 // int8 filter operand: per 32-row block scale s (127*s >= max |a_i|/|a| over the block),
 // q_i = rint(a_i/(|a| s)); ea_max (u32 bits of a non-negative float, atomicMax) receives
 // an upper bound of max_row || a/|a| - s q ||_2.
@@ -61,16 +50,15 @@ hipError_t launch_rows_to_i8(const float* rows, uint64_t n, uint64_t n_pad, uint
 hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim, uint32_t ld,
                                     int8_t* out, float* scales, hipStream_t s);
 // Query preparation: exact |b| (src/metrics.rs:155), flags, padded f32 copy, the filter
-// operand (bf16 or int8 + scale) and the per-query certification bound ebound[q].
+// operand (int8 + scale) and the per-query certification bound ebound[q].
 struct QueryPrepArgs {
     const float* q;        // caller's queries [nq][dim]
     uint32_t nq, qpad, dim, ld;
-    FilterOp op;
-    const uint32_t* ea_max;  // i8: row-side error bound (device word)
+    const uint32_t* ea_max;  // row-side error bound (device word)
     float* qf32;           // [qpad][ld]
     float* nb;             // [qpad]
-    void* qop;             // bf16 [qpad][ld] or int8 [qpad][ld]
-    float* qscale;         // i8: [qpad]
+    void* qop;             // int8 [qpad][ld]
+    float* qscale;         // [qpad]
     float* ebound;         // [qpad]
     uint32_t* qflags;      // [qpad]
     int32_t* qids;         // [qpad]: min(q, nq-1), the exact scan's query-id list
@@ -108,9 +96,9 @@ constexpr uint32_t kTailDiv = 8;
 constexpr uint32_t kTailCounters = 64;
 // e0 / e1 (optional): events recorded at the kernel's own dispatch and completion
 // (hipExtLaunchKernel), i.e. its device duration without the stream's launch gaps.
-hipError_t launch_filter_sample(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+hipError_t launch_filter_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                                 hipEvent_t e1 = nullptr);
-hipError_t launch_filter_emit(FilterOp op, const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+hipError_t launch_filter_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                               hipEvent_t e1 = nullptr);
 // int8 only, batches of <= 16 queries (query tile rows 0..15), HBM-bound: the same
 // contract as the two launches above.

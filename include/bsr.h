@@ -7,9 +7,11 @@
  * parallel search's root: see there); bsr_last_error() gives a thread-local message.  No
  * C++ exception or panic crosses this boundary.  Plain pointers only: query, row and
  * output pointers may be host or device (hipMalloc) memory, detected per call.
- * Device inputs: the library's streams are blocking streams, so its work waits for work
- * issued before the call on the legacy default (NULL) stream (e.g. PyTorch's default
- * stream); data produced on any other stream must be complete (synchronized) first.
+ * Device inputs: bsr_index_load / bsr_index_append synchronize the device before reading
+ * device rows (one-time calls).  The search entry points do not: the library's streams are
+ * blocking streams, so their work waits for work issued before the call on the legacy
+ * default (NULL) stream (e.g. PyTorch's default stream); queries produced on any other
+ * stream must be complete (synchronized) first.
  *
  * Each entry point names the reference item it replaces (paths relative to the reference
  * repository nichmorgan/better-search-rag-rust):
@@ -72,10 +74,12 @@ typedef struct {
 #define BSR_MAX_K 256u
 #define BSR_FLAG_EXACT_ONLY 1u /* never use the MFMA candidate stage (always full exact scan) */
 #define BSR_FLAG_PROFILE 2u    /* record per-kernel HIP events (bsr_index_profile) */
-/* MFMA candidate filter operand: int8 (default; v_mfma_i32_32x32x32_i8, per-32-row-block
- * and per-query scales, certified with a measured Cauchy-Schwarz bound) or bf16 with this
- * flag (v_mfma_f32_32x32x16_bf16, certified with a constant bound).  Either way every
- * returned list is exact; the filter only decides how much exact work a query needs. */
+/* The MFMA candidate filter's operand is int8 (v_mfma_i32_16x16x64_i8 for rows of up to 768
+ * bytes, v_mfma_i32_32x32x32_i8 otherwise; per-32-row-block and per-query scales, certified
+ * with a measured Cauchy-Schwarz bound).  Every returned list is exact; the filter only
+ * decides how much exact work a query needs.  The bf16 filter operand of earlier rounds is
+ * retired: bsr_index_create with this flag returns BSR_E_INVALID (a bf16 CORPUS, cfg.dtype =
+ * BSR_BF16, is served on the int8 filter). */
 #define BSR_FLAG_FILTER_BF16 4u
 
 /* Mirrors RankInterval {start_index, end_index} (load_balance.rs:8-17). end < start means
@@ -95,10 +99,11 @@ typedef struct {
     uint32_t n_fallback;       /* queries whose MFMA candidate set failed certification */
     uint32_t n_candidates;     /* k' candidates rescored per query */
     uint64_t n_emitted;        /* candidates emitted by the MFMA filter (all queries) */
-    uint32_t filter_op;        /* 0 = int8 filter, 1 = bf16 filter (BSR_FLAG_FILTER_BF16) */
-    float row_ebound;          /* int8: max over rows of ||a/|a| - s q||_2 (0 for bf16) */
+    uint32_t filter_op;        /* 0 = int8 filter (the only operand since round 4) */
+    float row_ebound;          /* max over rows of ||a/|a| - s q||_2 (int8 quantisation) */
     uint32_t n_rescued;        /* queries certified by the second chance (all emitted rows) */
-    uint32_t graph_replay;     /* 1: the search replayed a captured hipGraph (small batches) */
+    uint32_t graph_replay;     /* 1: the search replayed a captured hipGraph (every filtered batch
+                                  from the second search of its shape on) */
 } bsr_search_stats;
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts
@@ -130,7 +135,8 @@ int bsr_index_create(const bsr_config* cfg, bsr_index** out);
 void bsr_index_destroy(bsr_index* ix);
 /* Copy n_rows row-major rows (f32, or bf16 bits when cfg.dtype == BSR_BF16) into HBM and
  * precompute per-row state.  global_offset is the global index of local row 0
- * (interval_by_rank(rank,size,N).start_index).  Replaces any previous contents. */
+ * (interval_by_rank(rank,size,N).start_index).  Replaces any previous contents.  Device rows
+ * may come from any stream: load and append synchronize the device before reading them. */
 int bsr_index_load(bsr_index* ix, const void* rows, uint64_t n_rows, uint64_t global_offset);
 /* Append rows after the current ones (PolarsVectorstore::append_many, polars.rs:101-119). */
 int bsr_index_append(bsr_index* ix, const void* rows, uint64_t n_rows);

@@ -7,7 +7,9 @@ offset), then calls bsr_parallel_top_k_similarity_search on the whole query batc
   normal     every rank searches;
   fail_last  the last rank's index has max_k < k, so its GPU search fails;
   fail_root  the same on rank 0;
-  shape      the last rank passes one query fewer (collective rejection).
+  shape      the last rank passes one query fewer (collective rejection);
+  hook_fault the last rank's header all-gather, issued from the search's hook, fails before it
+             is posted (BSR_INJECT_FAULT): the rank must still post it, with its error status.
 The rank writes {status, message, and on the root the lists} to <out>.rank<r>.npz.
 """
 import argparse
@@ -43,6 +45,8 @@ def main():
     a = ap.parse_args()
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(a.port)
+    if a.case == "hook_fault":
+        os.environ["BSR_INJECT_FAULT"] = f"header_hook:{a.world - 1}"
     import torch  # noqa: F401  (before libbsr: one HIP runtime per process, tests/conftest.py)
     import torch.distributed as dist
     import bsr

@@ -193,8 +193,23 @@ def _worker_collective_safety(rank, world, port, out_path):
         st2, msg2 = 0, ""
     except bsr.BsrError as e:
         st2, msg2 = e.status, str(e)
+    # gather_global_top_k: a malformed local list on one rank, then a batch size
+    # that differs on one rank -- every rank raises, before any list moves
+    li = np.zeros((4, K), np.uint64)
+    ld = np.zeros((4, K), np.float32)
+    lc = np.zeros(4, np.uint32)
+    msgs = []
+    for bad in ((li[:, :K - 1] if rank == 1 else li, ld, lc), (li[:3], ld[:3], lc[:3]) if rank == world - 1 else
+                (li, ld, lc)):
+        try:
+            bsr.gather_global_top_k(comm, *bad, K)
+            msgs.append("")
+        except bsr.BsrError as e:
+            msgs.append(str(e))
     dist.barrier()
     np.savez(f"{out_path}.{rank}.npz", st=st, st2=st2, msg2=np.frombuffer((msg2 or " ").encode(), np.uint8),
+             g1=np.frombuffer((msgs[0] or " ").encode(), np.uint8),
+             g2=np.frombuffer((msgs[1] or " ").encode(), np.uint8),
              warned=np.frombuffer((warned or " ").encode(), np.uint8),
              cnt=res[2] if res is not None else np.zeros(0, np.uint32), none=res is None)
     comm.close()
@@ -215,3 +230,8 @@ def test_gloo_parallel_search_collective_safety(tmp_path):
     # batch sizes that disagree: all ranks rejected, collectively
     for i in range(world):
         assert int(r[i]["st2"]) == -1 and b"disagree on the batch shape" in r[i]["msg2"].tobytes()
+    # gather_global_top_k: malformed lists on rank 1, then Q = 3 on the last rank: all raise
+    for i in range(world):
+        g1, g2 = r[i]["g1"].tobytes(), r[i]["g2"].tobytes()
+        assert (b"local lists must be" if i == 1 else b"rank(s) [1] passed invalid local lists") in g1, (i, g1)
+        assert b"disagree on the batch shape" in g2, (i, g2)

@@ -64,3 +64,25 @@ def test_bench_two_ranks_host_transport(gpu):
     assert d["exchange_ms_per_step"] is not None
     sc = d["parity_spot_check"]
     assert sc["indices_equal"] and sc["distance_bits_equal"]
+
+
+def _failing_run(extra=(), timeout=60):
+    """bench.py --gpus 2 with rank 1 failing on purpose (BSR_BENCH_FAIL_RANK): the launcher must
+    end rank 0 -- blocked in a collective with the dead rank -- and report, within the time."""
+    import time
+    env = dict(os.environ, BSR_BENCH_FAIL_RANK="1")
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "host",
+                        "--rows", "200000", *QUICK, *extra], cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    dt = time.monotonic() - t0
+    assert r.returncode != 0 and dt < timeout, (r.returncode, dt)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    d = json.loads(lines[-1])
+    assert d["value"] is None and d["failed_rank"] == 1 and "rank 1 exited with status 3" in d["error"]
+    assert "BSR_BENCH_FAIL_RANK" in d["stderr_tail"]
+    return d
+
+
+def test_bench_failing_rank_fails_fast(gpu):
+    _failing_run()

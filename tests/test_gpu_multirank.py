@@ -101,6 +101,18 @@ def test_parallel_search_failing_rank(bsr_mod, oracle_mod, gpu, corpus, tmp_path
     assert int(res[0]["idx"][2, 0]) != mr_worker.N - 1  # the last block's self-match is missing
 
 
+def test_parallel_search_header_hook_fault(bsr_mod, oracle_mod, gpu, corpus, tmp_path):
+    # a header collective that failed before it was posted must be posted again
+    # with the error status (no rank left blocked, no mismatched collectives)
+    world = 3
+    rows, q = corpus
+    res = _run(world, "hook_fault", tmp_path)
+    s_last = bsr_mod.interval_by_rank(world - 1, world, mr_worker.N).start_index
+    assert int(res[world - 1]["status"]) == -4 and b"injected fault" in res[world - 1]["msg"].tobytes()
+    assert int(res[1]["status"]) == 0 and int(res[0]["status"]) == 0
+    _same(res[0], _want(oracle_mod, rows, q, 0, s_last))
+
+
 def test_parallel_search_failing_root(bsr_mod, oracle_mod, gpu, corpus, tmp_path):
     world = 2
     rows, q = corpus

@@ -78,16 +78,11 @@ def test_golden_search(bsr_mod, gpu, exact_only):
             _assert_same((gi[sl], gd[sl], gc[sl]), want, f"case {ci} rep {r}")
 
 
-# ---- exact scan (small batches) and filter path (batches) vs the oracle --------------
-FILTERS = pytest.mark.parametrize("fflags", [0, 4], ids=["i8", "bf16"])  # 4 = BSR_FLAG_FILTER_BF16
-
-
-# ---- small batches: int8 skinny filter (bf16 index / k > 200: exact scan) vs the oracle --
-@FILTERS
+# ---- small batches: int8 skinny filter (k > 200: exact scan) vs the oracle -----------------
 @pytest.mark.parametrize("n,dim,nq,k", [
     (1, 768, 1, 10), (5, 768, 3, 10), (257, 768, 2, 1), (1000, 768, 5, 64), (3000, 130, 9, 100),
     (4097, 768, 4, 256), (20000, 768, 8, 50), (100000, 768, 16, 10), (70000, 96, 1, 10)])
-def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
+def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
     rng = np.random.default_rng(n + dim + k)
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
     if n > 10:
@@ -95,17 +90,16 @@ def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags
         rows[3] = 0
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
     qs[0] = rows[min(1, n - 1)]
-    ix = _index(bsr_mod, rows, flags=fflags)
+    ix = _index(bsr_mod, rows, flags=0)
     got = ix.local_top_k(qs, k)
     st = ix.last_stats()
-    if (fflags and nq < 16) or k > 200:
+    if k > 200:
         assert st.n_exact_direct == nq
     else:
         assert st.n_exact_direct == 0 and st.n_fallback == 0, (st.n_exact_direct, st.n_fallback)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
 
 
-@FILTERS
 @pytest.mark.parametrize("n,dim,nq,k", [
     (20000, 768, 32, 10),   # config 1 stand-in (JabRef ~20k chunks, 32 queries, top-10)
     (20000, 768, 40, 50),   # the reference's own k = 50 (src/main.rs:110)
@@ -116,7 +110,7 @@ def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags
     (5000, 40, 16, 10),     # 64-byte int8 rows: one K slice per tile
     (6000, 1100, 20, 10),   # rows longer than the rescore's LDS query copy (1024 floats)
 ])
-def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
+def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
     rng = np.random.default_rng(7 * n + k)
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
     rows[n - 1] = rows[0]            # duplicate pair far apart
@@ -125,31 +119,29 @@ def test_filter_path_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k, fflags):
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
     qs[0] = rows[0]
     qs[1] = rows[20]
-    ix = _index(bsr_mod, rows, flags=fflags)
+    ix = _index(bsr_mod, rows, flags=0)
     got = ix.local_top_k(qs, k)
     st = ix.last_stats()
     assert st.n_exact_direct == 0 and st.n_candidates >= k
-    assert st.filter_op == (1 if fflags else 0)
+    assert st.filter_op == 0
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, k), f"n={n} k={k}")
     # both copies of row 0 lead query 0's list at distance 0, smaller index first
     assert list(got[0][0, :2]) == [0, n - 1] and got[1][0, 0] == 0 and got[1][0, 1] == 0
 
 
-@FILTERS
-def test_filter_certifies_uniform_data(bsr_mod, oracle_mod, gpu, fflags):
+def test_filter_certifies_uniform_data(bsr_mod, oracle_mod, gpu):
     # Independent U(-1,1) queries over a U(-1,1) corpus (the bench's data): the filter must
     # certify every query (a broken filter would still be exact, through fallbacks).
     rng = np.random.default_rng(11)
     rows = rng.uniform(-1, 1, (60000, 768)).astype(np.float32)
     qs = rng.uniform(-1, 1, (48, 768)).astype(np.float32)
     qs[0] = rows[123]
-    ix = _index(bsr_mod, rows, flags=fflags)
+    ix = _index(bsr_mod, rows, flags=0)
     got = ix.local_top_k(qs, 10)
     st = ix.last_stats()
     assert st.n_fallback == 0 and st.n_exact_direct == 0, (st.n_fallback, st.n_exact_direct)
     assert st.n_emitted >= 48 * 64
-    if not fflags:
-        assert 1e-3 < st.row_ebound < 6e-3, st.row_ebound
+    assert 1e-3 < st.row_ebound < 6e-3, st.row_ebound
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "uniform")
 
 
@@ -183,8 +175,7 @@ def test_large_k_many_queries_dense_emission(bsr_mod, oracle_mod, gpu):
     _assert_same((gi[sub], gd[sub], gc[sub]), oracle_mod.parallel_top_k(rows, qs[sub], 100), "k=100 Q=2048")
 
 
-@FILTERS
-def test_duplicate_runs_overflow_lane_rings(bsr_mod, oracle_mod, gpu, fflags):
+def test_duplicate_runs_overflow_lane_rings(bsr_mod, oracle_mod, gpu):
     # Runs of 400 identical rows: a query equal to one of them passes the filter on a whole
     # run (64 rows per lane per tile, more than a lane's candidate ring); ties resolve by
     # index and every result stays exact (through the fallback when uncertifiable).
@@ -193,20 +184,19 @@ def test_duplicate_runs_overflow_lane_rings(bsr_mod, oracle_mod, gpu, fflags):
     rows = np.repeat(base, 400, axis=0)
     qs = base[rng.integers(0, 100, 40)].copy()
     qs[1::2] += rng.uniform(-0.05, 0.05, (20, 768)).astype(np.float32)
-    ix = _index(bsr_mod, rows, flags=fflags)
+    ix = _index(bsr_mod, rows, flags=0)
     got = ix.local_top_k(qs, 10)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "duplicate runs")
 
 
-@FILTERS
-def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu, fflags):
+def test_filter_path_normal_data_with_clusters(bsr_mod, oracle_mod, gpu):
     # Clustered embeddings (dense neighbourhoods) stress the certification; any query it
     # cannot certify must fall back to the exact scan and still be exact.
     rng = np.random.default_rng(42)
     centers = rng.normal(size=(20, 768)).astype(np.float32)
     rows = (centers[rng.integers(0, 20, 40000)] + 0.05 * rng.normal(size=(40000, 768))).astype(np.float32)
     qs = (centers[rng.integers(0, 20, 24)] + 0.05 * rng.normal(size=(24, 768))).astype(np.float32)
-    ix = _index(bsr_mod, rows, flags=fflags)
+    ix = _index(bsr_mod, rows, flags=0)
     got = ix.local_top_k(qs, 10)
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "clusters")
 
@@ -256,6 +246,37 @@ def test_append_many_then_search(bsr_mod, oracle_mod, gpu):
     _assert_same(ix.local_top_k(qs, 16), oracle_mod.parallel_top_k(rows, qs, 16), "append")
 
 
+def test_load_and_append_device_rows_from_side_stream(bsr_mod, oracle_mod, gpu):
+    """Device rows written on a torch side stream, not synchronized by the caller: load and
+    append must read the rows written (polars.rs:121-156 -- the slab read is the slab written),
+    not what the buffer held before."""
+    import torch
+    rng = np.random.default_rng(12)
+    n = 40000
+    rows = rng.uniform(-1, 1, (n, 768)).astype(np.float32)
+    src = torch.from_numpy(rows).cuda()
+    dst = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        delay = torch.randn(4096, 4096, device="cuda")
+        for _ in range(40):  # tens of ms of side-stream work ahead of the copies
+            delay = torch.tanh(delay @ delay)
+        dst[: n // 2].copy_(src[: n // 2])
+    ix = bsr_mod.Index(768, max_k=10, device=0)
+    ix.load(dst[: n // 2])  # no synchronisation by the caller
+    with torch.cuda.stream(side):
+        for _ in range(40):
+            delay = torch.tanh(delay @ delay)
+        dst[n // 2:].copy_(src[n // 2:])
+    ix.append_many(dst[n // 2:])
+    assert np.array_equal(ix.get_many(), rows)
+    qs = rng.uniform(-1, 1, (24, 768)).astype(np.float32)
+    qs[0] = rows[n - 5]
+    _assert_same(ix.local_top_k(qs, 10), oracle_mod.parallel_top_k(rows, qs, 10), "side stream")
+    torch.cuda.synchronize()
+
+
 def test_errors(bsr_mod, gpu):
     ix = bsr_mod.Index(768, max_k=10, device=0)
     with pytest.raises(bsr_mod.BsrError) as e:
@@ -303,6 +324,13 @@ def test_overflowing_rows_force_exact(bsr_mod, oracle_mod, gpu):
     got = ix.local_top_k(qs, 10)
     assert ix.last_stats().n_exact_direct == 20
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "overflow")
+
+
+def test_bf16_filter_operand_retired(bsr_mod, gpu):
+    # the bf16 filter OPERAND (rounds 1-3) is retired; a bf16 CORPUS is served on the int8 filter
+    with pytest.raises(bsr_mod.BsrError) as e:
+        bsr_mod.Index(768, max_k=10, device=0, flags=bsr_mod.BSR_FLAG_FILTER_BF16)
+    assert e.value.status == -1 and "retired" in str(e.value)
 
 
 def test_bf16_corpus_widened(bsr_mod, oracle_mod, gpu):

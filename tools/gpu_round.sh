@@ -1,33 +1,115 @@
 #!/bin/bash
-# Standard measurement pass on the GPU box (tooling): GPU parity tests, the default bench
-# (configs[2] corpus 10M x 1000, with the configs[1] side line), the configs[3] / configs[4]
-# benches, configs[1] and the 1.25M-row shard of an 8-GPU run, then rocprofv3 kernel stats of the default bench.
-# Every GPU step has its own time limit; a crash or time limit ends the script.
-# (The PMC passes are tools/gpu_r02p.sh; the filter A/B microbenchmark tools/microbench.)
-# usage: bash tools/gpu_round.sh TAG
+# GPU-box measurement passes (tooling), one launcher for every round's runs.
+#   usage: bash tools/gpu_round.sh TAG STEP [STEP ...]      (default steps: tests bench)
+# Steps (each GPU command under its own time limit; the first failure ends the script):
+#   tests       pytest -m gpu (the whole GPU suite)
+#   bench       the default bench (configs[2] corpus 10M x 1000 + the configs[1] side line)
+#   configs     configs[0] (c1, parquet store), configs[1] (c2), configs[3] (c4), configs[4] (c5)
+#   r125        the 1.25M-row shard of an 8-GPU split (the per-rank step of the scale curve)
+#   prof        rocprofv3 kernel stats of the default bench
+#   timeline    rocprofv3 kernel trace of the 1.25M shard -> per-batch kernel/gap timeline
+#   pmc         HBM traffic (FETCH_SIZE, WRITE_SIZE) at 10M / 5M / 2.5M / 1.25M rows into a copy of
+#               profiles/pmc_traffic.json, then one SQ/GRBM pass at 10M
+#   pmcsmall    two SQ passes (issue, LDS, waits) over the default bench
+#   rehearsal   --gpus 2 and 4 over the host transport on the one GPU (spawn, exchange, root merge)
+#   stamps      s_memtime phase split of the emit filter (make lab-fstamps) at 10M and 1.25M
+#   counters    emission-epilogue event counts + per-workgroup balance (make lab-counters)
+#   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
+#               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard
 TAG=${1:-run}
+shift
+STEPS=${*:-tests bench}
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 9
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p "$O"
+NOB="--no-cpu-baseline --no-configs1"
 
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 "$O/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
+run() {  # run SECONDS LABEL OUTFILE CMD...: one GPU step, its limit, its status
+    local t=$1 label=$2 out=$3
+    shift 3
+    timeout -k 10 "$t" "$@" > "$out" 2>> "$O/err.txt"
+    local rc=$?
+    echo "$label rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+}
 
-timeout -k 10 400 python bench.py > "$O/bench.json" 2> "$O/bench.err"
-rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_c4.json" 2>> "$O/bench.err"
-rc=$?; echo "bench c4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --config c5 --steps 5 --warmup 2 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_c5.json" 2>> "$O/bench.err"
-rc=$?; echo "bench c5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --config c1 --steps 50 --warmup 5 > "$O/bench_c1.json" 2>> "$O/bench.err"
-rc=$?; echo "bench c1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_c2.json" 2>> "$O/bench.err"
-rc=$?; echo "bench c2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 --no-cpu-baseline --no-configs1 > "$O/bench_125.json" 2>> "$O/bench.err"
-rc=$?; echo "bench 1.25M rc=$rc"; [ $rc -eq 0 ] || exit $rc
-
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
-    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --verify 0 --no-configs1 > "$O/bench_prof.json" 2> "$O/prof.err"
-rc=$?; echo "rocprof stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
+for step in $STEPS; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -3 "$O/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      run 400 bench "$O/bench.json" python bench.py; head -c 400 "$O/bench.json"; echo ;;
+    configs)
+      run 300 "bench c1" "$O/bench_c1.json" python bench.py --config c1 --steps 50 --warmup 5
+      run 300 "bench c2" "$O/bench_c2.json" python bench.py --config c2 --steps 20 --warmup 3 --verify 2 $NOB
+      run 300 "bench c4" "$O/bench_c4.json" python bench.py --config c4 --steps 5 --warmup 2 --verify 2 $NOB
+      run 300 "bench c5" "$O/bench_c5.json" python bench.py --config c5 --steps 5 --warmup 2 --verify 2 $NOB ;;
+    r125)
+      run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
+      head -c 400 "$O/bench_125.json"; echo ;;
+    prof)
+      run 300 "rocprof stats" "$O/bench_prof.json" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
+          python3 bench.py --steps 10 --warmup 3 --verify 0 $NOB
+      f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -12 "$f" ;;
+    timeline)
+      run 300 "trace 1.25M" "$O/bench_125_prof.json" rocprofv3 --kernel-trace --output-format csv -d "$O/tl125" -o run -- \
+          python3 bench.py --rows 1250000 --verify 0 --steps 30 --p50-iters 3 $NOB
+      f=$(find "$O/tl125" -name "*kernel_trace.csv" | head -1)
+      python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_125.txt"; tail -30 "$O/timeline_125.txt" ;;
+    pmc)
+      export PMC_RUN="$TAG"
+      cp profiles/pmc_traffic.json "$O/pmc_traffic.json"
+      B="python3 bench.py --steps 3 --warmup 1 --verify 0 --p50-iters 2 $NOB"
+      for rows in 10000000 5000000 2500000 1250000; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          run 240 "pmc $rows $c" /dev/null rocprofv3 --pmc $c --output-format csv -d "$O/t$rows/$c" -o run -- $B --rows $rows
+        done
+        python3 tools/pmc_traffic.py "$O/t$rows/FETCH_SIZE" "$O/t$rows/WRITE_SIZE" $rows 1000 i8 "$O/pmc_traffic.json" || exit 1
+      done
+      run 240 "pmc sq" /dev/null rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+          SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA --output-format csv -d "$O/sq/p1" -o run -- $B
+      run 240 "pmc grbm" /dev/null rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$O/sq/p2" -o run -- $B
+      python3 tools/microbench/pmc_summary.py "$O/sq" > "$O/pmc_summary.txt"
+      grep -A20 "qs16<true" "$O/pmc_summary.txt" | head -22 ;;
+    pmcsmall)
+      B="python3 bench.py --steps 3 --warmup 1 --verify 0 --p50-iters 2 $NOB"
+      run 240 "pmc small 1" /dev/null rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+          SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA --output-format csv -d "$O/ps/p1" -o run -- $B
+      run 240 "pmc small 2" /dev/null rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU \
+          SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE --output-format csv -d "$O/ps/p2" -o run -- $B
+      python3 tools/microbench/pmc_summary.py "$O/ps" > "$O/pmc_small_summary.txt" ;;
+    rehearsal)
+      for n in 2 4; do
+        run 400 "bench N=$n host" "$O/bench_n$n.json" python bench.py --gpus $n --comm host --steps 10 --warmup 2 --verify 2 \
+            --no-cpu-baseline
+        head -c 600 "$O/bench_n$n.json"; echo
+      done ;;
+    stamps)
+      for rows in 10000000 1250000; do
+        BSR_LIB=tools/ab/libbsr_fstamps.so run 240 "stamps $rows" "$O/stamps_$rows.txt" python tools/diag/filter_stamps.py $rows
+        grep -v amdgpu.ids "$O/stamps_$rows.txt"
+      done ;;
+    counters)
+      for rows in 10000000 1250000; do
+        BSR_LIB=tools/ab/libbsr_counters.so run 240 "counters $rows" "$O/counters_$rows.txt" python tools/diag/filter_counters.py $rows
+        cat "$O/counters_$rows.txt"
+        BSR_LIB=tools/ab/libbsr_counters.so run 240 "wg balance $rows" "$O/wg_$rows.txt" python tools/diag/filter_wg_balance.py $rows
+        cat "$O/wg_$rows.txt"
+      done ;;
+    ab:*|ab125:*)
+      extra=""; [ "${step%%:*}" = ab125 ] && extra="--rows 1250000 --steps 50"
+      for r in 1 2; do
+        for v in $(echo "${step#*:}" | tr , ' '); do
+          if [ "$v" = new ]; then L=""; else L="tools/ab/libbsr_$v.so"; fi
+          BSR_LIB=$L run 200 "${step%%:*} $v $r" "$O/${step%%:*}_${v}_$r.json" python bench.py --steps 30 --warmup 5 \
+              --verify 0 --p50-iters 5 $NOB $extra
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['emitted_per_query_rank0'])" \
+              "$O/${step%%:*}_${v}_$r.json" "$v"
+        done
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
 echo done
