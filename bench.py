@@ -339,10 +339,10 @@ def main():
     import torch
     import bsr
 
-    wd = Watchdog(rank) if world > 1 else None
+    watchdog = Watchdog(rank) if world > 1 else None
     dist = None
     if world > 1:
-        wd.arm("process group init", args.collective_timeout)
+        watchdog.arm("process group init", args.collective_timeout)
         import torch.distributed as dist
         # (gloo prints its connection report to stdout: keep stdout for the one JSON line)
         sys.stdout.flush()
@@ -353,7 +353,7 @@ def main():
         finally:
             os.dup2(saved_fd, 1)
             os.close(saved_fd)
-        wd.disarm()
+        watchdog.disarm()
     ndev = torch.cuda.device_count()
     device = local_rank % max(ndev, 1)
     torch.cuda.set_device(device)
@@ -365,14 +365,14 @@ def main():
         torch.cuda.synchronize()
         if dist:
             t = timeout or args.collective_timeout
-            prev = wd.save()
-            wd.arm("barrier", t + 30)
+            prev = watchdog.save()
+            watchdog.arm("barrier", t + 30)
             dist.monitored_barrier(timeout=timedelta(seconds=t))
-            wd.restore(prev)
+            watchdog.restore(prev)
 
     def armed(label):
-        if wd:
-            wd.arm(label, args.collective_timeout)
+        if watchdog:
+            watchdog.arm(label, args.collective_timeout)
 
     D, Q, K = args.dim, args.queries, args.k
     n_total = args.rows_total * (world if args.scaling == "weak" else 1)
@@ -719,8 +719,8 @@ def main():
     if rank == 0:
         out.setdefault("cpu_baseline", None)  # N > 1: the baseline is measured at N = 1 only
         print(json.dumps(out), flush=True)
-    if wd:
-        wd.disarm()
+    if watchdog:
+        watchdog.disarm()
     barrier(timeout=max(args.collective_timeout, 1200))  # (rank 0's spot-check and CPU sweep ran)
     if comm:
         comm.close()

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 namespace bsr {
 
@@ -466,6 +467,13 @@ __device__ __forceinline__ void qs_vm_n(int n) {  // (stamp build) s_waitcnt vmc
 #endif
 typedef __attribute__((ext_vector_type(4))) int i32x4v_t;
 
+// f(std::integral_constant<int, I>) for I = 0, 1, ...: a loop the compiler must unroll (the
+// emit filter's slice loop -- each slice's DMA, barrier and epilogue placement is a constant).
+template <class F, int... I>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
 constexpr int kSampleTilesPerWG = 8;  // sample pass (compact): tiles of maxima staged in LDS
 
 __device__ __forceinline__ uint32_t qs16_swz(uint32_t row) { return ((row >> 3) & 1u) * 2u; }
@@ -521,7 +529,11 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
         __builtin_amdgcn_sched_barrier(0);                                              \
     } while (0)
 #endif
-template <bool EMIT, int NK>
+// DEFER (lab): the emission epilogue in front of the next tile's first MFMAs -- 1.9% faster at
+// the 1.25M-row shard, 4% slower at tau = inf, even at 10M (profiles/r04b_fab_*.txt): not kept.
+// TAILX: the dynamic tail in 8 XCD-local pools (the product, tail = 1/8); 0 = one counter per
+// query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
+template <bool EMIT, int NK, bool DEFER = false, int TAILX = 8>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
     constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
@@ -560,19 +572,42 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr uint32_t kEnd = 0xFFFFFFFFu;
     constexpr bool kStaticSched = NK > A;
     const bool dyn = EMIT && kStaticSched && p.tail != nullptr && active;
-    const uint32_t n_st = dyn ? n_rt - n_rt / kTailDiv : n_rt;
+    const uint32_t n_st = dyn ? n_rt - n_rt / (TAILX ? TAILX : kTailDiv) : n_rt;
     const uint32_t my_static = (active && g0 < n_st) ? (n_st - 1 - g0) / RG + 1 : 0;
     // (one lane) claim the next tail tile of this query tile: the counter's old value, turned
     // into a tile id by tail_id() where it is consumed -- not at once, which would wait for the
     // atomic and, in order, for every DMA in flight.  The address is one the compiler cannot
     // prove uniform: the atomic optimizer would otherwise aggregate the atomic across the wave
     // and consume its result immediately.
+    // TAILX: the tail is split into 8 pools of consecutive tiles, pool x claimed first by the
+    // workgroups on XCD x (counter tail[x * n_qt + qt]), so that the n_qt workgroups reading a
+    // tail tile sit on one XCD and share it through its L2; a workgroup whose own pool is empty
+    // steals from the next XCD's pools (the balancing the tail exists for).  Without TAILX one
+    // counter per query tile hands every tail tile to workgroups of different XCDs.
+    const uint32_t n_tail = n_rt - n_st, pool_sz = (n_tail + 7) / 8;
+    uint32_t cpool = xcd, pools_tried = 1;  // (lane 0 of wave 0) the pool claimed from
+    auto pool_n = [&](uint32_t x) -> uint32_t {
+        const uint32_t lo = x * pool_sz;
+        return lo >= n_tail ? 0u : min(pool_sz, n_tail - lo);
+    };
     auto claim_raw = [&]() -> uint32_t {
         uint32_t z;
         asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-        return atomicAdd(p.tail + qt + z, 1u);
+        return atomicAdd(p.tail + (TAILX ? cpool * p.n_qt : 0u) + qt + z, 1u);
     };
-    auto tail_id = [&](uint32_t v) -> uint32_t { return n_st + v < n_rt ? n_st + v : kEnd; };
+    auto tail_id = [&](uint32_t v) -> uint32_t {
+        if constexpr (!TAILX) {
+            return n_st + v < n_rt ? n_st + v : kEnd;
+        } else {
+            for (;;) {  // (own pool empty: claim from the next XCD's, synchronously -- rare)
+                if (v < pool_n(cpool)) return n_st + cpool * pool_sz + v;
+                if (pools_tried == 8) return kEnd;
+                ++pools_tried;
+                cpool = (cpool + 1) & 7;
+                v = atomicAdd(p.tail + cpool * p.n_qt + qt, 1u);
+            }
+        }
+    };
     auto claim = [&]() -> uint32_t { return tail_id(claim_raw()); };
 
     // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
@@ -653,6 +688,45 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     };
 
     i32x4v_t acc[8][2];
+    // (DEFER) the emission epilogue of the PREVIOUS tile, one 32-row pair at a time (row blocks
+    // 2s, 2s+1: one block scale), placed in front of the next tile's first MFMAs on those row
+    // blocks, whose C = 0 operand overwrites them: the lane's maximum per query block, scored
+    // once, one ballot per pair; a pair that passes appends its passing rows as level 2 does.
+    // Its VALU work runs beside the partner wave's MFMAs instead of in a tile-end phase that
+    // every wave of the workgroup reaches together.
+    auto epi_pair = [&](int s, float scs, uint32_t rte) {
+        int bm[2][2];
+        bool pass = false;
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const i32x4v_t& x = acc[2 * s + h][nb];
+                bm[h][nb] = max(max(x[0], x[1]), max(x[2], x[3]));
+            }
+            const int m = max(bm[0][nb], bm[1][nb]);
+            pass |= ((float)m * scs) * sbq[nb] >= tau[nb];
+        }
+        if (!__ballot(pass)) return;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                if (!__ballot(((float)bm[h][nb] * scs) * sbq[nb] >= tau[nb])) continue;
+                if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) flush_ring(nb);  // room for 4 rows
+                const i32x4v_t& x = acc[2 * s + h][nb];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = ((float)x[r] * scs) * sbq[nb];
+                    const uint32_t row = rte * BM + (2 * s + h) * 16 + 4 * (lane >> 4) + r;
+                    lkeys[(nb * CAP + ecnt[nb]) * NT] = score_key(v, row);
+                    ecnt[nb] += (v >= tau[nb] && row < p.n_rows) ? 1u : 0u;
+                }
+            }
+        }
+    };
+    float sc_prev[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+    uint32_t rt_prev = 0;
     // the first two tiles of the sequence
     uint32_t cur_id = my_rt ? g0 : kEnd, nxt_id = my_rt > 1 ? g0 + RG : kEnd;
     if (dyn && my_static < 2) {
@@ -697,7 +771,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     unsigned long long fst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_a, st_b, st_loop0;
     BSR_FST(st_loop0);
 #endif
-    for (uint32_t t = 0; cur_id != kEnd; ++t) {
+    uint32_t t = 0;
+    for (; cur_id != kEnd; ++t) {
         const uint32_t rt = cur_id;
         BSR_FCNT(4);
         if (kStatic && t) {
@@ -719,12 +794,20 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         // it leaves the DMA stream's vmcnt waits alone)
         float sc_tile = 1.0f;
         if constexpr (!EMIT) sc_tile = p.a_scale[rt * BM / kSampleScaleRows];
-#pragma unroll
-        for (int kt = 0; kt < NK; ++kt) {
+        static_for(std::make_integer_sequence<int, NK>{}, [&](auto KT) {
+            constexpr int kt = decltype(KT)::value;
             const uint32_t jj = t * NK + kt;
             const bool bar_slice = (kt & 1) == 1;
 #pragma unroll
             for (int rb = 0; rb < 8; ++rb) {
+                if constexpr (DEFER && EMIT && kt == 0) {
+                    if ((rb & 1) == 0 && t > 0) epi_pair(rb >> 1, sc_prev[rb >> 1], rt_prev);
+                    // pin the first MFMAs on these row blocks below the epilogue (their C = 0
+                    // operand does not read the accumulators, so nothing else orders them, and
+                    // hoisted above it they would need a second set of accumulators)
+                    asm volatile("" : "+v"(fa[rb & 3]));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
                     if (kt == 0) {
@@ -770,7 +853,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-        }
+        });
         // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
         const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
         bool stored = false;
@@ -820,6 +903,12 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 }
                 stored = true;
             }
+        } else if constexpr (DEFER) {
+            // (the epilogue runs in front of the next tile's first MFMAs, or after the loop)
+            // (held in VGPRs: the loop's scalar registers are spoken for)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(sc_prev[i]) : "s"(sc[i]));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(rt_prev) : "s"(rt));
         } else {
             // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
             // each query block, scored with the tile's largest (or, for a negative maximum,
@@ -895,6 +984,11 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
         cur_id = nxt_id;
         nxt_id = req ? __builtin_amdgcn_readfirstlane(lds_ids[t & 1]) : n2;
+    }
+    if constexpr (DEFER && EMIT) {  // the last tile's epilogue
+        if (t > 0)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) epi_pair(s, sc_prev[s], rt_prev);
     }
     wait_vm0();  // the stream's trailing DMAs land before the workgroup ends
 #ifdef BSR_FILTER_STAMPS
@@ -1135,7 +1229,8 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
     const uint32_t q = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
-    if (q == 0 && t < (int)kTailCounters) cnt[qpad + t] = 0;  // the emit filter's tail counters
+    if (q == 0)  // the emit filter's tail counters
+        for (uint32_t i = t; i < 8 * kTailCounters; i += blockDim.x) cnt[qpad + i] = 0;
     if (q >= qpad) return;
     if (t == 0) cnt[q] = 0;
     if (q >= nq || (qflags[q] & kQueryNoApprox)) {

@@ -90,8 +90,8 @@ struct GemmArgs {
     // tile from tail[qt] (zeroed by k_select_tau); tail = nullptr: every tile static
     uint32_t* tail;
 };
-// Dynamic tail of the emit filter: 1/kTailDiv of the row tiles; counters per query tile
-// (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + qt].
+// Dynamic tail of the emit filter: 1/kTailDiv of the row tiles; counters per (XCD pool, query
+// tile) (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + x * n_qt + qt].
 constexpr uint32_t kTailDiv = 8;
 constexpr uint32_t kTailCounters = 64;
 // e0 / e1 (optional): events recorded at the kernel's own dispatch and completion

@@ -14,6 +14,8 @@
 #   rehearsal   --gpus 2 and 4 over the host transport on the one GPU (spawn, exchange, root merge)
 #   stamps      s_memtime phase split of the emit filter (make lab-fstamps) at 10M and 1.25M
 #   counters    emission-epilogue event counts + per-workgroup balance (make lab-counters)
+#   fab         tools/microbench/filter_ab (product vs variants of the emit filter) at 10M and 1.25M
+#   fabpmc      FETCH_SIZE of each filter_ab variant at 10M and 1.25M (HBM traffic per launch)
 #   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
 #               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard
 TAG=${1:-run}
@@ -97,6 +99,15 @@ for step in $STEPS; do
         cat "$O/counters_$rows.txt"
         BSR_LIB=tools/ab/libbsr_counters.so run 240 "wg balance $rows" "$O/wg_$rows.txt" python tools/diag/filter_wg_balance.py $rows
         cat "$O/wg_$rows.txt"
+      done ;;
+    fab)
+      run 300 "filter_ab 10M" "$O/fab_10m.txt" tools/microbench/filter_ab 10000000 1000 10 0.1473; cat "$O/fab_10m.txt"
+      run 200 "filter_ab 1.25M" "$O/fab_125.txt" tools/microbench/filter_ab 1250000 1000 30 0.1284; cat "$O/fab_125.txt" ;;
+    fabpmc)
+      for rows in 10000000 1250000; do
+        run 300 "filter_ab pmc $rows" /dev/null rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fabpmc_$rows" -o run -- \
+            tools/microbench/filter_ab $rows 1000 2 0.1473
+        python3 tools/microbench/pmc_summary.py "$O/fabpmc_$rows" > "$O/fabpmc_$rows.txt"; grep -A2 "qs16" "$O/fabpmc_$rows.txt"
       done ;;
     ab:*|ab125:*)
       extra=""; [ "${step%%:*}" = ab125 ] && extra="--rows 1250000 --steps 50"
