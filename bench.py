@@ -601,9 +601,11 @@ def main():
                 "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank)" +
                                ("" if world == 1 else f" + {args.comm.upper()} all-gather of the partial lists"
                                                       " + root merge"),
-                "filter": ("int8 MFMA (v_mfma_i32_16x16x64_i8) candidates" if args.filter == "i8" else
-                           "bf16 MFMA (v_mfma_f32_32x32x16_bf16) candidates") +
-                          f", exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)",
+                "filter": "int8 MFMA (v_mfma_i32_16x16x64_i8) candidates, " + (
+                    f"exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)"
+                    if st.n_candidates else
+                    "emission threshold selected from every rank's sample (all-gathered), exact sequential-f32 "
+                    "rescore of every emitted row, the merged lists certified on every rank (DESIGN.md §6)"),
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
             "p50_config": f"1 query over {n_total} rows on {world} GPU(s)" + (
@@ -626,7 +628,7 @@ def main():
                 "local_search_total": round(prof_scan.search_ms / max(prof_scan.searches, 1), 4)},
             "fallback_queries_per_step_rank0": stats_fb / args.steps,
             "rescued_queries_per_step_rank0": stats_rescued / args.steps,
-            "candidates_per_query": st.n_candidates,
+            "candidates_per_query": st.n_candidates,  # (0: global threshold, every emitted row rescored)
             "self_query_rank1": bool(res_i[0, 0] == 0 and res_d[0, 0] == 0.0),
             "emitted_per_query_rank0": round(st.n_emitted / max(Q, 1), 1),
             "row_ebound": round(float(st.row_ebound), 6),

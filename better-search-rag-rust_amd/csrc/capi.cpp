@@ -97,11 +97,15 @@ struct bsr_comm {
     DevBuf hdr_send, hdr_recv;     // the parallel search's shape agreement (RCCL)
     PinnedVec<int32_t> h_hdr;      // [1 + size][kHdrWords]: this rank's words, then every rank's
     bool hdr_posted = false;       // this search's header all-gather has been issued
+    // the global-threshold search (parallel_gtau): gathered sample keys, gathered result
+    // buffers, the merged result (device and pinned host), the fallback queries
+    DevBuf g_smax, g_res, m_res, fb_q;
+    PinnedVec<uint8_t> h_mres, h_stage;
 };
 
 // The parallel search's header, all-gathered before the lists: every rank's batch shape
 // and local status, so that no rank issues a list exchange the others do not match.
-constexpr size_t kHdrWords = 4;  // {n_queries, k, local status, magic}
+constexpr size_t kHdrWords = 8;  // {n_queries, k, local status, magic, gtau, rows lo, rows hi, 0}
 constexpr int32_t kHdrMagic = 0x42535231;
 
 // Copy to a caller buffer that may be host or device memory.
@@ -538,22 +542,22 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
     BSR_GUARD(gather_global_impl(comm, local_idx, local_dist, local_count, n_queries, k, out_idx, out_dist, out_count));
 }
 
-// All-gather of every rank's header {nq, k, status of the local checks, magic} into
-// c->h_hdr[1 + r]: through the host transport (synchronous), or as a 16-byte RCCL all-gather
-// on c->stream that header_wait() completes -- enqueued before the local search, so its
-// latency hides behind the search.
+// All-gather of every rank's header {nq, k, status of the local checks, magic, global-threshold
+// capable, shard rows} into c->h_hdr[1 + r]: through the host transport (synchronous), or as a
+// 32-byte RCCL all-gather on c->stream that header_wait() completes.
 // Fault injection for the collective-safety tests (BSR_INJECT_FAULT=header_hook[:rank]): the
-// header all-gather issued from the search's hook fails before it is posted, as a buffer that
-// cannot be sized would make it fail.
-static bool inject_header_hook_fault(const bsr_comm* c) {
+// first header all-gather of a search fails before it is posted, as a buffer that cannot be
+// sized would make it fail; the rank must then post it again with its error status.
+static bool inject_header_fault(const bsr_comm* c) {
     static const char* v = getenv("BSR_INJECT_FAULT");
     if (!v || strncmp(v, "header_hook", 11) != 0) return false;
     return v[11] != ':' || atoi(v + 12) == c->rank;
 }
 
-static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool from_hook = false) {
+static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool gtau, uint64_t n_rows,
+                        bool first = false) {
     const size_t P = (size_t)c->size, hb = kHdrWords * sizeof(int32_t);
-    if (from_hook && inject_header_hook_fault(c))
+    if (first && inject_header_fault(c))
         return set_error(BSR_E_NOMEM, "injected fault: header buffers (BSR_INJECT_FAULT)");
     BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));
     int32_t* h = c->h_hdr.data();
@@ -561,6 +565,10 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool f
     h[1] = (int32_t)k;
     h[2] = st;
     h[3] = kHdrMagic;
+    h[4] = gtau ? 1 : 0;
+    h[5] = (int32_t)(uint32_t)n_rows;
+    h[6] = (int32_t)(uint32_t)(n_rows >> 32);
+    h[7] = 0;
     if (c->host_fn) {
         c->hdr_posted = true;  // (a failing transport fails on every rank)
         if (c->host_fn(h, h + kHdrWords, hb, c->host_user) != 0)
@@ -580,21 +588,187 @@ static int header_wait(bsr_comm* c) {
     if (!c->host_fn) BSR_HIP(stream_wait(c->stream));
     return BSR_OK;
 }
+static const int32_t* header_of(const bsr_comm* c, int32_t r) {
+    return c->h_hdr.data() + kHdrWords * (1 + (size_t)r);
+}
+
+// An all-gather of `bytes` device bytes per rank on `stream` (RCCL), or through the host
+// transport (staged through pinned memory: a host round trip).
+static int allgather_device(bsr_comm* c, const void* send, void* recv, size_t bytes, hipStream_t stream) {
+    if (!c->host_fn) {
+        BSR_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c->comm, stream));
+        return BSR_OK;
+    }
+    const size_t P = (size_t)c->size;
+    BSR_TRY(c->h_stage.resize(bytes * (1 + P)));
+    uint8_t* hs = c->h_stage.data();
+    BSR_HIP(hipMemcpyAsync(hs, send, bytes, hipMemcpyDeviceToHost, stream));
+    BSR_HIP(stream_wait(stream));
+    if (c->host_fn(hs, hs + bytes, bytes, c->host_user) != 0)
+        return set_error(BSR_E_RCCL, "host all-gather callback failed");
+    BSR_HIP(hipMemcpyAsync(recv, hs + bytes, bytes * P, hipMemcpyHostToDevice, stream));
+    return BSR_OK;
+}
+
+static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
+                         uint64_t* out_idx, float* out_dist, uint32_t* out_count, bool allow_gtau);
+
+// The rest of a parallel search with the global emission threshold, every rank
+// having enqueued phase A (query prep, sample pass, its ks best sample keys per query) and
+// every header saying so:
+//   1. all-gather of the sample keys -> phase B: the global tau (the threshold one shard of the
+//      whole corpus would select), the emit pass, the exact rescore of every emitted row, the
+//      rank's top-k of them with its exclusion bound per query;
+//   2. all-gather of the packed result buffers (lists, status words, bounds);
+//   3. EVERY rank merges them (compute_global_top_k, :141-171) and certifies the merged lists
+//      against the ranks' bounds -- the same deterministic kernel on the same bytes, so every
+//      rank knows the same uncertified set F;
+//   4. F (usually empty) takes the standard parallel search (local certified searches, their
+//      exchange and merge), collectively, and its rows replace the root's.
+// RCCL: every step is enqueued behind phase A on the index's stream, one host wait at the end.
+static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
+                         uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
+    const uint32_t P = (uint32_t)c->size;
+    const bool root = c->rank == 0;
+    hipStream_t s = ix->stream;
+    uint64_t n_total = 0;
+    for (int32_t r = 0; r < c->size; ++r) {
+        const int32_t* h = header_of(c, r);
+        n_total += (uint64_t)(uint32_t)h[5] | ((uint64_t)(uint32_t)h[6] << 32);
+    }
+    uint32_t need = (uint64_t)k < n_total ? k : (uint32_t)n_total;
+    {  // (test hook, BSR_INJECT_FAULT=gtau_uncertified: no merged list certifies -- F is every query)
+        static const char* v = getenv("BSR_INJECT_FAULT");
+        if (v && strcmp(v, "gtau_uncertified") == 0) need = k + 1;
+    }
+    BSR_HIP(hipSetDevice(ix->device));
+    // 1. the sample keys of every rank, then phase B
+    const size_t kb = (size_t)ix->gt_qpad * ix->gt_ks * sizeof(uint64_t);
+    BSR_TRY(c->g_smax.ensure(kb * P));
+    BSR_TRY(allgather_device(c, ix->smax.p, c->g_smax.p, kb, s));
+    BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P));
+    // 2. the packed result buffers
+    const size_t rbytes = ix->res_bytes;
+    BSR_TRY(c->g_res.ensure(rbytes * P));
+    BSR_TRY(allgather_device(c, ix->res[ix->cur].p, c->g_res.p, rbytes, s));
+    // 3. merge + certify into m_res: [fail count, NaN word | status words [P][4] | fail list
+    //    [nq] | counts [nq] | distances [nq][k] | indices [nq][k]]
+    const size_t nqk = (size_t)nq * k;
+    const size_t o_st = 16, o_fail = round_up(o_st + (size_t)P * kStWords * 4, 16),
+                 o_cnt = round_up(o_fail + (size_t)nq * 4, 16), o_dist = round_up(o_cnt + (size_t)nq * 4, 16),
+                 o_idx = round_up(o_dist + nqk * 4, 16), mbytes = o_idx + nqk * 8;
+    BSR_TRY(c->m_res.ensure(mbytes));
+    BSR_TRY(c->h_mres.resize(mbytes));
+    uint8_t* md = c->m_res.as<uint8_t>();
+    BSR_HIP(hipMemsetAsync(md, 0, 4, s));         // fail count
+    BSR_HIP(hipMemsetAsync(md + 4, 0xff, 4, s));  // the lowest query with a NaN distance: none
+    const uint8_t* g = c->g_res.as<uint8_t>();
+    MergeArgs ma{};
+    ma.idx = reinterpret_cast<const uint64_t*>(g + ix->res_off_idx);
+    ma.dist = reinterpret_cast<const float*>(g + ix->res_off_dist);
+    ma.cnt = reinterpret_cast<const uint32_t*>(g + ix->res_off_cnt);
+    ma.idx_stride = rbytes / 8;
+    ma.dist_stride = rbytes / 4;
+    ma.cnt_stride = rbytes / 4;
+    ma.P = P;
+    ma.nq = nq;
+    ma.k_in = k;
+    ma.k = k;
+    ma.out_idx = reinterpret_cast<uint64_t*>(md + o_idx);
+    ma.out_dist = reinterpret_cast<float*>(md + o_dist);
+    ma.out_count = reinterpret_cast<uint32_t*>(md + o_cnt);
+    ma.first_nan = reinterpret_cast<uint32_t*>(md) + 1;
+    ma.excl = reinterpret_cast<const float*>(g + ix->res_off_x);
+    ma.excl_stride = rbytes / 4;
+    ma.need = need;
+    ma.fail_cnt = reinterpret_cast<uint32_t*>(md);
+    ma.fail_list = reinterpret_cast<uint32_t*>(md + o_fail);
+    ma.st = reinterpret_cast<const uint32_t*>(g);
+    ma.st_stride = rbytes / 4;
+    ma.st_all = reinterpret_cast<uint32_t*>(md + o_st);
+    BSR_HIP(launch_merge(ma, s));
+    uint8_t* hm = c->h_mres.data();
+    BSR_HIP(hipMemcpyAsync(hm, md, mbytes, hipMemcpyDeviceToHost, s));
+    BSR_HIP(stream_wait(s));
+    bsr_index_collect_profile_impl(ix);
+    const uint32_t* hw = reinterpret_cast<const uint32_t*>(hm);
+    const uint32_t* st_all = reinterpret_cast<const uint32_t*>(hm + o_st);
+    ix->stats.n_emitted = st_all[(size_t)c->rank * kStWords + kStEmitted];
+    ix->stats.n_candidates = 0;  // (every emitted row was rescored)
+    for (uint32_t r = 0; r < P; ++r)
+        if (st_all[(size_t)r * kStWords + kStQueryFlags] & kQueryNonFinite)
+            return set_error(BSR_E_NONFINITE, "a query contains NaN/Inf (the reference panics; rank %u)", r);
+    if (hw[1] != ~0u) return set_error(BSR_E_NONFINITE, "NaN distance in query %u (the reference panics)", hw[1]);
+    // 4. the uncertified queries, collectively (every rank holds the same F)
+    const uint32_t nf = hw[0];
+    ix->stats.n_fallback = nf;
+    uint32_t* m_cnt = reinterpret_cast<uint32_t*>(hm + o_cnt);
+    float* m_dist = reinterpret_cast<float*>(hm + o_dist);
+    uint64_t* m_idx = reinterpret_cast<uint64_t*>(hm + o_idx);
+    if (nf) {
+        std::vector<uint32_t> fl(reinterpret_cast<const uint32_t*>(hm + o_fail),
+                                 reinterpret_cast<const uint32_t*>(hm + o_fail) + nf);
+        std::sort(fl.begin(), fl.end());
+        const uint32_t d = ix->dim;
+        const float* fq = nullptr;
+        std::vector<float> hq;
+        if (is_device_ptr(queries)) {
+            BSR_TRY(c->fb_q.ensure((size_t)nf * d * sizeof(float)));
+            for (uint32_t i = 0; i < nf; ++i)
+                BSR_HIP(hipMemcpyAsync(c->fb_q.as<float>() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float),
+                                       hipMemcpyDeviceToDevice, s));
+            BSR_HIP(stream_wait(s));
+            fq = c->fb_q.as<float>();
+        } else {
+            hq.resize((size_t)nf * d);
+            for (uint32_t i = 0; i < nf; ++i) memcpy(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float));
+            fq = hq.data();
+        }
+        std::vector<uint64_t> fi((size_t)nf * k);
+        std::vector<float> fd((size_t)nf * k);
+        std::vector<uint32_t> fc(nf);
+        const bsr_search_stats keep = ix->stats;
+        const int r = parallel_impl(c, ix, fq, nf, k, fi.data(), fd.data(), fc.data(), false);
+        ix->stats.n_emitted = keep.n_emitted;
+        ix->stats.n_fallback = nf;
+        ix->stats.n_queries = nq;
+        if (r != BSR_OK) return r;
+        if (root)
+            for (uint32_t i = 0; i < nf; ++i) {
+                const uint32_t q = fl[i];
+                m_cnt[q] = fc[i];
+                memcpy(m_idx + (size_t)q * k, fi.data() + (size_t)i * k, k * sizeof(uint64_t));
+                memcpy(m_dist + (size_t)q * k, fd.data() + (size_t)i * k, k * sizeof(float));
+            }
+    }
+    if (!root) return clear_counts(out_count, nq);
+    if (is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count)) {
+        BSR_HIP_OR_HOST_COPY(out_idx, m_idx, nqk * sizeof(uint64_t));
+        BSR_HIP_OR_HOST_COPY(out_dist, m_dist, nqk * sizeof(float));
+        BSR_HIP_OR_HOST_COPY(out_count, m_cnt, (size_t)nq * sizeof(uint32_t));
+    } else {
+        memcpy(out_idx, m_idx, nqk * sizeof(uint64_t));
+        memcpy(out_dist, m_dist, nqk * sizeof(float));
+        memcpy(out_count, m_cnt, (size_t)nq * sizeof(uint32_t));
+    }
+    return BSR_OK;
+}
 
 // parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206).  Collective-safe:
 // every rank reaches the same collectives whatever fails locally.
-//   1. local checks; (size > 1) the all-gather of every rank's header {nq, k, status} is
-//      enqueued; then compute_local_top_k on this rank's shard (:185);
-//   2. (size > 1) the headers: if the ranks disagree on the batch shape, EVERY rank returns
-//      BSR_E_INVALID and no list exchange happens (mismatched all-gathers are undefined);
-//   3. gather_top_k_results (:194): a rank whose search or checks failed contributes an empty
-//      list, as the reference's error branch does (:185-191);
-//   4. the root's merge (:200-202).
+//   1. local checks; (size > 1) the rank's eligibility for the global threshold and, when
+//      eligible, phase A enqueued; the all-gather of every rank's header {nq, k, status,
+//      eligible, shard rows}; ranks that disagree on the batch shape all return BSR_E_INVALID
+//      and no list exchange happens (mismatched all-gathers are undefined);
+//   2. every rank eligible and fine: the global-threshold search (parallel_gtau);
+//   3. otherwise compute_local_top_k (:185) on each rank, gather_top_k_results (:194) -- a rank
+//      whose search or checks failed contributes an empty list, as the reference's error
+//      branch does (:185-191) -- and the root's merge (:200-202).
 // Returns: BSR_OK; on a non-root rank whose local step failed, that error; on a root whose
 // own local step failed but whose outputs are usable, BSR_PARTIAL with the other ranks'
 // global top-k in out_* (the reference's root returns Some(..) there, :199-202).
 static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
-                         uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
+                         uint64_t* out_idx, float* out_dist, uint32_t* out_count, bool allow_gtau) {
     const bool root = !c || c->rank == 0;
     const bool outs_ok = !nq || (out_idx && out_dist && out_count);
     int st = BSR_OK;
@@ -602,26 +776,45 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     else if (root && !outs_ok) st = set_error(BSR_E_INVALID, "null output");
     else if (c && !c->host_fn && c->device != ix->device)
         st = set_error(BSR_E_INVALID, "communicator and index on different devices");
-    // the shape agreement's all-gather, issued right after the local search's GPU work is
-    // enqueued (its latency hides behind the search; issued first, its RCCL kernel would hold
-    // CUs the persistent filter needs); the header carries the local checks' status
     const bool multi = c && c->size > 1;
-    struct HookCtx { bsr_comm* c; uint32_t nq, k; int32_t st; } hc{c, nq, k, st};
-    auto hook = [](void* p) -> int {
-        const HookCtx* h = static_cast<const HookCtx*>(p);
-        return header_start(h->c, h->nq, h->k, h->st, true);
-    };
-    if (c) c->hdr_posted = false;
-    // compute_local_top_k (:185-191)
-    if (st == BSR_OK) {
-        st = ix->search_device(queries, nq, k, multi ? +hook : nullptr, &hc);
-        // (a failed header all-gather is a transport error: every rank sees it; report it)
-        if (multi && c->hdr_posted && st == BSR_E_RCCL) return st;
+    if (multi) {
+        // global threshold: this rank's filter path with a sample pass, lists the device merge
+        // takes, and the library setting (BSR_GLOBAL_TAU=0 turns it off)
+        static const bool gtau_on = [] {
+            const char* v = getenv("BSR_GLOBAL_TAU");
+            return !(v && v[0] == '0');
+        }();
+        bool gt = allow_gtau && gtau_on && st == BSR_OK && ix->gtau_eligible(nq, k) &&
+                  device_merge_fits((uint32_t)c->size, k, k);
+        if (gt) {
+            const int r = ix->gtau_phase_a(queries, nq, k);  // (enqueued: the header overlaps it)
+            if (r != BSR_OK) { st = r; gt = false; }
+        }
+        c->hdr_posted = false;
+        const int hs = header_start(c, nq, k, st, gt, ix ? ix->n : 0, true);
+        if (hs != BSR_OK && c->hdr_posted) return hs;  // (a transport error: every rank sees it)
+        if (!c->hdr_posted) {  // not posted: post it once more, carrying this failure
+            if (st == BSR_OK) st = hs;
+            gt = false;
+            BSR_TRY(header_start(c, nq, k, st, false, ix ? ix->n : 0));
+        }
+        BSR_TRY(header_wait(c));
+        const int32_t* h0 = header_of(c, 0);
+        bool all_gt = true;
+        for (int32_t r = 0; r < c->size; ++r) {
+            const int32_t* hr = header_of(c, r);
+            if (hr[3] != kHdrMagic || hr[0] != h0[0] || hr[1] != h0[1])
+                return set_error(BSR_E_INVALID,
+                                 "ranks disagree on the batch shape: rank 0 (n_queries %d, k %d), rank %d "
+                                 "(n_queries %d, k %d); no rank exchanged lists",
+                                 h0[0], h0[1], r, hr[0], hr[1]);
+            all_gt &= hr[4] == 1 && hr[2] == BSR_OK;
+        }
+        if (all_gt) return parallel_gtau(c, ix, queries, nq, k, out_idx, out_dist, out_count);
+        if (gt) BSR_HIP(stream_wait(ix->stream));  // (phase A ran for nothing: the standard path)
     }
-    // The header collective must be posted exactly once whatever failed before it (the search,
-    // or the hook itself before its all-gather: a buffer it could not size): then it carries
-    // this rank's error status, so the peers are never left in a collective this rank skipped.
-    if (multi && !c->hdr_posted) BSR_TRY(header_start(c, nq, k, st));
+    // compute_local_top_k (:185-191)
+    if (st == BSR_OK) st = ix->search_device(queries, nq, k);
     if (!c) {  // one rank, no communicator: the local lists are the result
         BSR_TRY(st);
         if (!nq) return BSR_OK;
@@ -631,18 +824,6 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     }
     std::string local_err;
     if (st != BSR_OK) local_err = last_error_cstr();
-    if (multi) {
-        BSR_TRY(header_wait(c));
-        const int32_t* h = c->h_hdr.data() + kHdrWords;
-        for (int32_t r = 0; r < c->size; ++r) {
-            const int32_t* hr = h + (size_t)r * kHdrWords;
-            if (hr[3] != kHdrMagic || hr[0] != h[0] || hr[1] != h[1])
-                return set_error(BSR_E_INVALID,
-                                 "ranks disagree on the batch shape: rank 0 (n_queries %d, k %d), rank %d "
-                                 "(n_queries %d, k %d); no rank exchanged lists",
-                                 h[0], h[1], r, hr[0], hr[1]);
-        }
-    }
     if (!nq) return st;
     if (k == 0) return st != BSR_OK ? st : set_error(BSR_E_INVALID, "k must be >= 1");
     const bool ok = st == BSR_OK;
@@ -689,7 +870,7 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
 
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries, uint32_t n_queries,
                                          uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
-    BSR_GUARD(parallel_impl(comm, ix, queries, n_queries, k, out_idx, out_dist, out_count));
+    BSR_GUARD(parallel_impl(comm, ix, queries, n_queries, k, out_idx, out_dist, out_count, true));
 }
 
 // ---------------------------------------------------------------------------------------

@@ -379,21 +379,22 @@ static int run_exact_scan_list(bsr_index* ix, const std::vector<int32_t>& ids, u
 static uint32_t kp_for(uint32_t k) { return 64u * ((3u * k + 34u + 63u) / 64u) - 1u; }
 static uint32_t cap_for(uint32_t k) { return 16u * (kp_for(k) + 1u); }
 
-// Candidate stage (steps 2-5) for every query of the batch.  Batches of at most 16
-// queries on an int8 index use the skinny (HBM-bound, no LDS) filter kernels.
-static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint32_t* next_status) {
-    const bool skinny = nq <= kSkinnyMaxQ;
+static uint32_t ks_for(uint32_t k) { return (kp_for(k) + 1u) / 8u; }
+
+// Steps 2-3 of the candidate stage: the sample pass and tau0 (smax: also the ks best sample
+// keys per query, the input of a parallel search's global threshold), then the emit pass.
+// Batches of at most 16 queries use the skinny (HBM-bound, no LDS) filter kernels.
+static int sample_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint64_t* smax);
+static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k);
+
+
+// Buffers of the candidate stage for a batch (k' = kp_for(k) candidates, lists of cap keys).
+static int filter_buffers(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     // k' candidates, (k'+1) % 64 == 0, about 3k: the k-th exact score must clear the (k'+1)-th
     // approximate one by E_q, and in a Gaussian-like tail that takes ~3x as many rows at
     // E_q/sigma ~ 0.26.  63 for k <= 10, 191 for k = 50, 383 for k = 100.
     const uint32_t kp = kp_for(k);
-    const uint32_t cap = 16u * (kp + 1u);
-    // (k'+1)/8: about 8 x 32 = 256 rows reach tau0 for k <= 10.  Fewer (ks = (k'+1)/12, /16)
-    // measured 1-2% less filter time and up to 1.3% of the queries falling back to the exact
-    // scan (profiles/r02f_*): not worth it.
-    const uint32_t ks = (kp + 1u) / 8u;
-    const uint32_t BM = kFilterTile;
-    const uint64_t n = ix->n;
+    const uint32_t cap = cap_for(k);
     ix->stats.n_candidates = kp;
     BSR_TRY(ix->tau.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(ix->cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
@@ -403,7 +404,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));
     BSR_TRY(ix->fail.ensure((size_t)nq * sizeof(uint32_t)));
     BSR_TRY(ix->fail2.ensure((size_t)nq * sizeof(uint32_t)));
+    return BSR_OK;
+}
 
+static GemmArgs gemm_args(bsr_index* ix, uint32_t qpad) {
     GemmArgs g{};
     g.A = ix->fop.as<uint8_t>();
     g.B = ix->qop.as<uint8_t>();
@@ -411,8 +415,21 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     g.n_qt = qpad / kFilterTile;
     g.a_scale = ix->ascale.as<float>();
     g.b_scale = ix->qscale.as<float>();
-    uint32_t* status = ix->d_status;
+    return g;
+}
 
+static int sample_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint64_t* smax) {
+    BSR_TRY(filter_buffers(ix, nq, qpad, k));
+    const bool skinny = nq <= kSkinnyMaxQ;
+    const uint32_t cap = cap_for(k);
+    // (k'+1)/8: about 8 x 32 = 256 rows reach tau0 for k <= 10.  Fewer (ks = (k'+1)/12, /16)
+    // measured 1-2% less filter time and up to 1.3% of the queries falling back to the exact
+    // scan (profiles/r02f_*): not worth it.
+    const uint32_t ks = ks_for(k);
+    const uint32_t BM = kFilterTile;
+    const uint64_t n = ix->n;
+    GemmArgs g = gemm_args(ix, qpad);
+    uint32_t* status = ix->d_status;
     if (n > cap) {
         // tau0 from every 32nd row: the ks-th best sampled score, or (large shards) the
         // ks-th best maximum over 32 sampled rows -- never above the former, so at least
@@ -437,28 +454,43 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
                           : launch_filter_sample(g, ix->stream, e0, e1);
         }, 2));
         BSR_HIP(launch_select_tau(ix->S.as<float>(), s_ld, n_vals, nq, qpad, ix->qflags.as<uint32_t>(), ks,
-                                  ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream));
+                                  ix->tau.as<float>(), ix->cnt.as<uint32_t>(), status, ix->stream, smax));
     } else {
         BSR_HIP(launch_select_tau(nullptr, 0, 0, nq, qpad, ix->qflags.as<uint32_t>(), ks, ix->tau.as<float>(),
-                                  ix->cnt.as<uint32_t>(), status, ix->stream));
+                                  ix->cnt.as<uint32_t>(), status, ix->stream, smax));
     }
-    g.A = ix->fop.as<uint8_t>();
+    return BSR_OK;
+}
+
+static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
+    const bool skinny = nq <= kSkinnyMaxQ;
+    const uint32_t BM = kFilterTile;
+    const uint64_t n = ix->n;
+    GemmArgs g = gemm_args(ix, qpad);
     g.a_stride = ix->op_row_bytes;
-    g.a_scale = ix->ascale.as<float>();
     g.a_scale_rows = kQuantBlock;
     g.n_rows = (uint32_t)n;
     g.n_rt = (uint32_t)((n + BM - 1) / BM);
-    g.S = nullptr;
     g.tau = ix->tau.as<float>();
     g.cand = ix->cand.as<uint64_t>();
     g.cnt = ix->cnt.as<uint32_t>();
-    g.cap = cap;
+    g.cap = cap_for(k);
     // the last 1/kTailDiv of the row tiles are balanced dynamically (k_filter_qs16)
     g.tail = g.n_qt <= kTailCounters ? ix->cnt.as<uint32_t>() + qpad : nullptr;
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return skinny ? launch_filter_skinny_emit(g, ix->stream, e0, e1)
                       : launch_filter_emit(g, ix->stream, e0, e1);
     }));
+    return BSR_OK;
+}
+
+// Candidate stage (steps 2-5) for every query of the batch.
+static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint32_t* next_status) {
+    BSR_TRY(sample_pass(ix, nq, qpad, k, nullptr));
+    BSR_TRY(emit_pass(ix, nq, qpad, k));
+    const uint32_t kp = kp_for(k);
+    const uint32_t cap = cap_for(k);
+    uint32_t* status = ix->d_status;
     // lists of <= 1024 keys (k <= 10): the rescore kernel selects its own k' candidates
     const bool fused_select = cap <= kFusedSelectCap;
     if (!fused_select) {
@@ -491,7 +523,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     ra.res_dist = ix->d_dist;
     ra.res_cnt = ix->d_cnt;
     ra.offset = ix->global_offset;
-    ra.n_rows = n;
+    ra.n_rows = ix->n;
     if (fused_select) {
         ra.sel = 1;
         ra.cand_keys = ix->cand.as<uint64_t>();
@@ -527,22 +559,15 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     return BSR_OK;
 }
 
-int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*),
-                             void* ctx) {
-    bsr_index* ix = this;
-    if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
-    if (k == 0 || k > ix->cfg.max_k) return set_error(BSR_E_INVALID, "k=%u outside [1, max_k=%u]", k, ix->cfg.max_k);
-    BSR_HIP(hipSetDevice(ix->device));
-    stats = bsr_search_stats{};
-    stats.n_queries = nq;
-    stats.filter_op = 0;  // int8
-    stats.row_ebound = row_ebound;
-    // packed result layout for this batch
+// The packed result buffer of a batch (status words | counts | distances | indices | the
+// global-threshold search's exclusion bounds), double-buffered; d_* point into res[cur].
+int bsr_index::prepare_result(uint32_t nq, uint32_t k) {
     const size_t nqk = (size_t)std::max(nq, 1u) * k;
     res_off_cnt = 16;
     res_off_dist = round_up(res_off_cnt + (size_t)std::max(nq, 1u) * sizeof(uint32_t), 16);
     res_off_idx = round_up(res_off_dist + nqk * sizeof(float), 16);
-    res_bytes = res_off_idx + nqk * sizeof(uint64_t);
+    res_off_x = round_up(res_off_idx + nqk * sizeof(uint64_t), 16);
+    res_bytes = round_up(res_off_x + (size_t)std::max(nq, 1u) * sizeof(float), 16);
     if (res[0].bytes < res_bytes || res[1].bytes < res_bytes) {
         for (DevBuf& r : res) {
             BSR_TRY(r.ensure(res_bytes));
@@ -564,9 +589,24 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     d_cnt = reinterpret_cast<uint32_t*>(rb + res_off_cnt);
     d_dist = reinterpret_cast<float*>(rb + res_off_dist);
     d_idx = reinterpret_cast<uint64_t*>(rb + res_off_idx);
-    uint32_t* next_status = res[cur ^ 1u].as<uint32_t>();
+    d_x = reinterpret_cast<float*>(rb + res_off_x);
     if (!next_status_clean) BSR_HIP(hipMemsetAsync(d_status, 0, kStWords * sizeof(uint32_t), stream));
     next_status_clean = false;
+    return BSR_OK;
+}
+
+int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*),
+                             void* ctx) {
+    bsr_index* ix = this;
+    if (!ix->loaded) return set_error(BSR_E_STATE, "index not loaded");
+    if (k == 0 || k > ix->cfg.max_k) return set_error(BSR_E_INVALID, "k=%u outside [1, max_k=%u]", k, ix->cfg.max_k);
+    BSR_HIP(hipSetDevice(ix->device));
+    stats = bsr_search_stats{};
+    stats.n_queries = nq;
+    stats.filter_op = 0;  // int8
+    stats.row_ebound = row_ebound;
+    BSR_TRY(prepare_result(nq, k));
+    uint32_t* next_status = res[cur ^ 1u].as<uint32_t>();
     if (nq == 0) return BSR_OK;
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
 
@@ -722,6 +762,105 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
             BSR_TRY(finalize_and_read());
         }
     }
+    return BSR_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// The parallel search's global emission threshold: phase A / phase B
+// ---------------------------------------------------------------------------------------
+bool bsr_index::gtau_eligible(uint32_t nq, uint32_t k) const {
+    // the filter path with a sample pass (a shard of more rows than one query's candidate list)
+    return loaded && nq > 0 && k >= 1 && k <= cfg.max_k && k <= kMaxKForFilter && approx_ok && n > cap_for(k);
+}
+
+int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
+    bsr_index* ix = this;
+    if (!gtau_eligible(nq, k)) return set_error(BSR_E_STATE, "global-threshold search not applicable");
+    if (!queries) return set_error(BSR_E_INVALID, "null queries");
+    BSR_HIP(hipSetDevice(device));
+    stats = bsr_search_stats{};
+    stats.n_queries = nq;
+    stats.row_ebound = row_ebound;
+    BSR_TRY(prepare_result(nq, k));
+    const uint32_t qpad = (uint32_t)round_up(nq, kFilterTile);
+    const uint32_t ks = ks_for(k);
+    BSR_TRY(qf32.ensure((size_t)qpad * ld * sizeof(float)));
+    BSR_TRY(nb.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(qop.ensure((size_t)qpad * op_row_bytes));
+    BSR_TRY(qscale.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(ebound.ensure((size_t)qpad * sizeof(float)));
+    BSR_TRY(qflags.ensure((size_t)qpad * sizeof(uint32_t)));
+    BSR_TRY(qids_id.ensure((size_t)qpad * sizeof(int32_t)));
+    BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
+    BSR_TRY(smax.ensure((size_t)qpad * ks * sizeof(uint64_t)));
+    const float* qsrc = queries;
+    if (!is_device_ptr(queries)) {
+        BSR_TRY(q_in.ensure((size_t)nq * dim * sizeof(float)));
+        BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
+        qsrc = q_in.as<float>();
+    }
+    QueryPrepArgs qa{};
+    qa.q = qsrc;
+    qa.nq = nq;
+    qa.qpad = qpad;
+    qa.dim = dim;
+    qa.ld = ld;
+    qa.ea_max = flags.as<uint32_t>() + 1;
+    qa.qf32 = qf32.as<float>();
+    qa.nb = nb.as<float>();
+    qa.qop = qop.p;
+    qa.qscale = qscale.as<float>();
+    qa.ebound = ebound.as<float>();
+    qa.qflags = qflags.as<uint32_t>();
+    qa.qids = qids_id.as<int32_t>();
+    qa.status = d_status;
+    qa.with_op = true;
+    BSR_HIP(launch_query_prep(qa, stream));
+    BSR_TRY(sample_pass(ix, nq, qpad, k, smax.as<uint64_t>()));
+    gt_nq = nq;
+    gt_k = k;
+    gt_qpad = qpad;
+    gt_ks = ks;
+    return BSR_OK;
+}
+
+int bsr_index::gtau_phase_b(const uint64_t* g_smax, uint32_t P) {
+    bsr_index* ix = this;
+    const uint32_t nq = gt_nq, k = gt_k, qpad = gt_qpad;
+    BSR_HIP(launch_global_tau(g_smax, P, qpad, nq, gt_ks, qflags.as<uint32_t>(), tau.as<float>(), stream));
+    BSR_TRY(emit_pass(ix, nq, qpad, k));
+    // every emitted row rescored exactly, one wave per query (mode B); the list is this rank's
+    // contribution, its exclusion bound goes with it (the root certifies the merged lists)
+    ev_begin(ix, ev_rescore);
+    RescoreArgs ra{};
+    ra.rows = rows.as<float>();
+    ra.ld = ld;
+    ra.dim = dim;
+    ra.na = na.as<float>();
+    ra.qf32 = qf32.as<float>();
+    ra.nb = nb.as<float>();
+    ra.n_items = nq;
+    ra.cand_keys = cand.as<uint64_t>();
+    ra.cnt = cnt.as<uint32_t>();
+    ra.cap = cap_for(k);
+    ra.tau0 = tau.as<float>();
+    ra.kp = kp_for(k);
+    ra.k = k;
+    ra.ebound = ebound.as<float>();
+    ra.out_keys = keys.as<uint64_t>();
+    ra.res_idx = d_idx;
+    ra.res_dist = d_dist;
+    ra.res_cnt = d_cnt;
+    ra.offset = global_offset;
+    ra.n_rows = n;
+    ra.excl_out = d_x;
+    ra.next_status = res[cur ^ 1u].as<uint32_t>();
+    ra.emit_cnt = cnt.as<uint32_t>();
+    ra.cur_status = d_status;
+    ra.n_queries = nq;
+    BSR_HIP(launch_rescore(ra, stream));
+    ev_end(ix, ev_rescore);
+    next_status_clean = true;
     return BSR_OK;
 }
 

@@ -93,11 +93,12 @@ struct bsr_index {
     size_t h_res_bytes = 0;
     uint32_t cur = 0;          // result buffer of the last search
     bool next_status_clean = false;  // status words of res[cur ^ 1] are known to be zero
-    size_t res_off_cnt = 0, res_off_dist = 0, res_off_idx = 0, res_bytes = 0;
+    size_t res_off_cnt = 0, res_off_dist = 0, res_off_idx = 0, res_off_x = 0, res_bytes = 0;
     uint32_t* d_status = nullptr;
     uint32_t* d_cnt = nullptr;
     float* d_dist = nullptr;
     uint64_t* d_idx = nullptr;
+    float* d_x = nullptr;      // global-threshold search: per-query exclusion bounds
 
     std::vector<uint32_t> h_qflags, h_fail;
 
@@ -129,4 +130,18 @@ struct bsr_index {
     // its shape-agreement collective there); its non-OK status is returned after the wait.
     int search_device(const float* queries, uint32_t nq, uint32_t k, int (*after_launch)(void*) = nullptr,
                       void* ctx = nullptr);
+    int prepare_result(uint32_t nq, uint32_t k);
+
+    // Parallel search with a global emission threshold (P > 1), in two halves
+    // around the all-gather of every rank's ks best sample keys:
+    //   phase A: query prep, the sample pass, tau0 and the keys (smax [qpad][gt_ks]);
+    //   phase B: the global threshold from the gathered keys g[P][qpad][gt_ks], the emit pass
+    //            and the exact rescore of EVERY emitted row, its top-k written as the result
+    //            rows with the per-query exclusion bound d_x (no local certification).
+    // Both enqueue only (no host wait).  gtau_eligible: the filter path with a sample pass.
+    bool gtau_eligible(uint32_t nq, uint32_t k) const;
+    int gtau_phase_a(const float* queries, uint32_t nq, uint32_t k);
+    int gtau_phase_b(const uint64_t* g_smax, uint32_t P);
+    bsr::DevBuf smax;
+    uint32_t gt_nq = 0, gt_k = 0, gt_qpad = 0, gt_ks = 0;
 };

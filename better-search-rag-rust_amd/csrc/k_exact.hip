@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     float* const lds = lds_all + w * STAGE;
     float* const ldq_all = lds_all + W * STAGE;
     const uint32_t n_items = a.n_items_dev ? *a.n_items_dev : a.n_items;
-    if (W > 1 && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
+    if ((W > 1 || a.excl_out) && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
         // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
         if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
         uint32_t sum = 0;
@@ -339,7 +339,21 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         if (w == 0) {
             L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
             bool certified = false;
-            if (lane == 0) {
+            if (a.excl_out) {
+                // (global threshold: the root certifies; this rank reports its exclusion bound)
+                if (lane == 0) {
+                    const float tx = overflow ? INFINITY : a.tau0[q];
+                    const double eb = (double)a.ebound[q];
+                    double x;
+                    if (tx == -INFINITY) x = INFINITY;  // every row of the shard was a candidate
+                    else if (!(tx < INFINITY) || !(eb < 1.0) || !((double)tx < 1.0 - eb - 1e-4 - 6e-9 / (double)mag_b))
+                        x = -INFINITY;
+                    else x = 1.0 - (double)tx - eb - 2.5e-7;
+                    float xf = (float)x;
+                    if ((double)xf > x) xf = nextafterf(xf, -INFINITY);  // (rounded down)
+                    a.excl_out[q] = xf;
+                }
+            } else if (lane == 0) {
                 // Certification: every row outside the candidate set has
                 // approximate cosine <= tau_x, hence reference cosine <= tau_x + E_q and
                 // reference distance >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must
@@ -366,8 +380,8 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             }
             // fused finalize: certified lists (modes S / A) and every second-chance item (mode
             // B) become result rows now; the first pass's uncertified ones are left to mode B
-            if (a.res_idx && (W > 1 || __shfl((int)certified, 0, kWave))) {
-                const uint32_t cnt = (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
+            if (a.res_idx && (W > 1 || a.excl_out || __shfl((int)certified, 0, kWave))) {
+                const uint32_t cnt = a.excl_out ? min(a.k, c) : (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
                     const uint32_t i = e * kWave + lane;
@@ -583,24 +597,29 @@ __global__ void k_finalize(const uint64_t* __restrict__ keys, uint32_t nq, uint3
 // smaller key is dropped (the HashSet keeps first occurrences), and the k smallest keys left
 // are the result.  Rows past out_count[q] are (~0, +inf), as merge_top_k_lists writes them.
 // A NaN distance: out_count[q] = 0 and the lowest such q in *first_nan (the reference panics).
+// (MergeArgs: list l of query q at idx + l * idx_stride + q * k_in, dist likewise, its count
+// at cnt[l * cnt_stride + q]; with excl, the certification of a parallel search with a global
+// threshold, and the lists' status words copied out -- kernels.hpp.)
 template <int E>
-__global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__ idx,
-                                                    const float* __restrict__ dist,
-                                                    const uint32_t* __restrict__ cnt, uint32_t P,
-                                                    uint32_t nq, uint32_t k_in, uint32_t k,
-                                                    uint64_t* __restrict__ out_idx,
-                                                    float* __restrict__ out_dist,
-                                                    uint32_t* __restrict__ out_count,
-                                                    uint32_t* __restrict__ first_nan) {
+__global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
+    const uint64_t* __restrict__ idx = a.idx;
+    const float* __restrict__ dist = a.dist;
+    const uint32_t P = a.P, nq = a.nq, k_in = a.k_in, k = a.k;
+    uint64_t* __restrict__ out_idx = a.out_idx;
+    float* __restrict__ out_dist = a.out_dist;
+    uint32_t* __restrict__ out_count = a.out_count;
     __shared__ uint64_t s_idx[kMergeMaxEntries];
     __shared__ uint64_t s_key[kMergeMaxEntries];
     __shared__ float s_dist[kMergeMaxEntries];
     __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
+    if (a.st_all && q == 0)  // every list's status words, compact
+        for (uint32_t i = lane; i < P * kStWords; i += kWave)
+            a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
     if (q >= nq) return;
     // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
-    const uint32_t c_l = lane < (int)P ? min(cnt[(uint64_t)lane * nq + q], k_in) : 0u;
+    const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
     uint32_t incl = c_l;
 #pragma unroll
     for (int off = 1; off < kWave; off <<= 1) {
@@ -613,11 +632,12 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
     for (uint32_t l = 0; l < P; ++l) {
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, (int)l);
         const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)l);
-        const uint64_t base = ((uint64_t)l * nq + q) * k_in;
+        const uint64_t bi = (uint64_t)l * a.idx_stride + (uint64_t)q * k_in;
+        const uint64_t bd = (uint64_t)l * a.dist_stride + (uint64_t)q * k_in;
         for (uint32_t i = lane; i < c; i += kWave) {
-            const float d = dist[base + i];
+            const float d = dist[bd + i];
             nan |= d != d;
-            s_idx[o + i] = idx[base + i];
+            s_idx[o + i] = idx[bi + i];
             s_dist[o + i] = d;
             s_key[o + i] = ((uint64_t)ord_f32(d + 0.0f) << 32) | (o + i);  // (-0.0 + 0.0 = +0.0)
         }
@@ -628,7 +648,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
     if (__ballot(nan)) {
         if (lane == 0) {
             out_count[q] = 0;
-            atomicMin(first_nan, q);
+            atomicMin(a.first_nan, q);
         }
         for (uint32_t p = lane; p < k; p += kWave) {
             oi[p] = ~0ull;
@@ -700,6 +720,26 @@ __global__ __launch_bounds__(64) void k_merge_lists(const uint64_t* __restrict__
         }
     }
     if (lane == 0) out_count[q] = got;
+    const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
+    if (a.excl && lane == 0) {
+        // Certification of a global-threshold parallel search: every row left
+        // out on rank l lies at a distance >= excl_l[q] (its kernel's bound, rounded down), so
+        // the merged list is the reference's iff it holds need = min(k, corpus rows) entries and
+        // its k-th distance lies strictly below every rank's bound (a shorter list only when
+        // every row of the corpus was a candidate: every bound +inf).
+        float xmin = INFINITY;
+        for (uint32_t l = 0; l < P; ++l) {
+            const float x = a.excl[(uint64_t)l * a.excl_stride + q];
+            xmin = x == x ? fminf(xmin, x) : -INFINITY;
+        }
+        bool ok = got >= a.need;
+        if (ok && got == k) {
+            ok = (double)s_dist[(uint32_t)kth] < (double)xmin;
+        } else if (ok) {
+            ok = xmin == INFINITY;
+        }
+        if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
+    }
 }
 
 // src/metrics.rs:143-165 for one pair (single lane, fully sequential, from global memory).
@@ -812,11 +852,28 @@ hipError_t launch_finalize(const uint64_t* keys, uint32_t nq, uint32_t k, uint64
 hipError_t launch_merge_lists(const uint64_t* idx, const float* dist, const uint32_t* cnt, uint32_t P, uint32_t nq,
                               uint32_t k_in, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count,
                               uint32_t* first_nan, hipStream_t s) {
+    MergeArgs a{};
+    a.idx = idx;
+    a.dist = dist;
+    a.cnt = cnt;
+    a.idx_stride = a.dist_stride = (uint64_t)nq * k_in;
+    a.cnt_stride = nq;
+    a.P = P;
+    a.nq = nq;
+    a.k_in = k_in;
+    a.k = k;
+    a.out_idx = out_idx;
+    a.out_dist = out_dist;
+    a.out_count = out_count;
+    a.first_nan = first_nan;
+    return launch_merge(a, s);
+}
+hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
+    const uint32_t P = a.P, nq = a.nq, k_in = a.k_in, k = a.k;
     if (P > (uint32_t)kWave || (uint64_t)P * k_in > kMergeMaxEntries || k > 4 * kWave) return hipErrorInvalidValue;
     const uint32_t e = (k + 63) / 64;
 #define BSR_MLISTS(E)                                                                                \
-    hipLaunchKernelGGL(k_merge_lists<E>, dim3(nq), dim3(64), 0, s, idx, dist, cnt, P, nq, k_in, k, out_idx, \
-                       out_dist, out_count, first_nan)
+    hipLaunchKernelGGL(k_merge_lists<E>, dim3(nq), dim3(64), 0, s, a)
     switch (e) {
         case 1: BSR_MLISTS(1); break;
         case 2: BSR_MLISTS(2); break;

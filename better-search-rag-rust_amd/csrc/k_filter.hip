@@ -533,13 +533,20 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 // the 1.25M-row shard, 4% slower at tau = inf, even at 10M (profiles/r04b_fab_*.txt): not kept.
 // TAILX: the dynamic tail in 8 XCD-local pools (the product, tail = 1/8); 0 = one counter per
 // query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
-template <bool EMIT, int NK, bool DEFER = false, int TAILX = 8>
+template <bool EMIT, int NK, int EPI = 0, int TAILX = 8>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
+    constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
     constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
     constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
     constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
-    constexpr int EM_BYTES = EMIT ? NT * 2 * CAP * 8 : 0;
+    // STAGE: per-query LDS lists [BN][QCAP] keys + counts, the stage of raw blocks [NSTG][1 KiB]
+    // + their records [NSTG][4 words], the queries' {scale, tau} [BN][2], the stage count
+    constexpr int QCAP = 32, NSTG = 16;
+    constexpr int ST_QL = 0, ST_STG = ST_QL + BN * QCAP * 8, ST_META = ST_STG + NSTG * 1024,
+                  ST_QPAR = ST_META + NSTG * 16, ST_QCNT = ST_QPAR + BN * 8, ST_CNT = ST_QCNT + BN * 4,
+                  ST_BYTES = ST_CNT + 16;
+    constexpr int EM_BYTES = !EMIT ? 0 : STAGE ? ST_BYTES : NT * 2 * CAP * 8;
     // SAMPLE, compact: the workgroup's maxima [tile][4][256 queries], written to S at the end
     constexpr int SB_BYTES = EMIT ? 0 : kSampleTilesPerWG * 4 * BN * 4;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[S * SLOT + EM_BYTES + SB_BYTES + 16];
@@ -638,6 +645,58 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         __builtin_amdgcn_s_waitcnt(0x0F70);
     };
 
+    // STAGE: emission balanced over the workgroup's waves.  A wave whose tile passes level 1
+    // copies each passing 16-row x 16-query block's raw accumulators (1 KiB) to the stage with
+    // a record {first row, first query, block scale}; after the next tile's first barrier EVERY
+    // wave scores a 1/8 share of the staged values (one per thread) and appends the passing
+    // (score, row) keys to per-query LDS lists (an LDS atomic per key), flushed to the global
+    // lists at the end.  The emitting wave no longer holds the workgroup at the next barrier
+    // while it appends (the level-2 skew of the per-lane rings: DESIGN.md §5).
+    uint8_t* const est = lds + S * SLOT;
+    uint64_t* const st_ql = reinterpret_cast<uint64_t*>(est + ST_QL);
+    int* const st_blk = reinterpret_cast<int*>(est + ST_STG);
+    uint32_t* const st_meta = reinterpret_cast<uint32_t*>(est + ST_META);
+    float* const st_qpar = reinterpret_cast<float*>(est + ST_QPAR);
+    uint32_t* const st_qcnt = reinterpret_cast<uint32_t*>(est + ST_QCNT);
+    uint32_t* const st_cnt = reinterpret_cast<uint32_t*>(est + ST_CNT);
+    // one value of a staged or inline block: query ql of the tile (local), corpus row `row`
+    auto st_append = [&](int iv, float scb, uint32_t row, uint32_t ql) {
+        const float v = ((float)iv * scb) * st_qpar[2 * ql];
+        if (v >= st_qpar[2 * ql + 1] && row < p.n_rows) {
+            uint32_t pos;
+            const uint32_t addr = (uint32_t)(uintptr_t)(st_qcnt + ql);
+            asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(pos) : "v"(addr), "v"(1u) : "memory");
+            if (pos < (uint32_t)QCAP) {
+                st_ql[ql * QCAP + pos] = score_key(v, row);
+            } else {  // (list full: straight to the global list)
+                const uint32_t q = qt * BN + ql;
+                const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v, row);
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): keep the DMA stream's counted waits exact
+            }
+        }
+    };
+    // every thread: the staged values v = tid, tid + 512, ... of n staged blocks
+    auto st_process = [&](uint32_t n) {
+        for (uint32_t v = tid; v < n * 256; v += NT) {
+            const uint32_t e = v >> 8, i = v & 255, l = i >> 2;
+            const int iv = st_blk[v];
+            const uint32_t* m = st_meta + 4 * e;
+            st_append(iv, __uint_as_float(m[2]), m[0] + 4 * (l >> 4) + (i & 3), m[1] + (l & 15));
+        }
+    };
+    if constexpr (STAGE) {
+        if (lane < 16)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const uint32_t ql = w * 32 + nb * 16 + lane;
+                st_qpar[2 * ql] = sbq[nb];
+                st_qpar[2 * ql + 1] = tau[nb];
+            }
+        if (tid < BN) st_qcnt[tid] = 0;
+        if (tid == 0) *st_cnt = 0;
+    }
+
     // LDS-DMA: wave w fills rows 16w .. 16w+15 of each slice (1 KiB per instruction); the
     // source chunk is XOR-swizzled so that LDS chunk position p holds global chunk p ^ swz.
     const uint32_t lrow = w * 16 + (lane >> 2);
@@ -727,6 +786,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     };
     float sc_prev[4] = {1.0f, 1.0f, 1.0f, 1.0f};
     uint32_t rt_prev = 0;
+    uint32_t n_stg = 0;  // (STAGE) the previous tile's staged block count
     // the first two tiles of the sequence
     uint32_t cur_id = my_rt ? g0 : kEnd, nxt_id = my_rt > 1 ? g0 + RG : kEnd;
     if (dyn && my_static < 2) {
@@ -851,6 +911,18 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 #endif
                     qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
                 }
+                if constexpr (STAGE) {
+                    // the previous tile's stage: its count read after the kt = 1 barrier (every
+                    // wave's stage writes landed before it), the values scored at kt = 2 (the
+                    // count's read long complete), the count reset after the kt = 3 barrier (every
+                    // wave has read it); the next stage writes follow the kt = 11 barrier
+                    if (kt == 1 && rb == 5) n_stg = min(*st_cnt, (uint32_t)NSTG);
+                    if (kt == 2 && rb == 0 && n_stg) st_process(n_stg);
+                    if (kt == 3 && rb == 5 && tid == 0) {
+                        *st_cnt = 0;
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         });
@@ -902,6 +974,64 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                     }
                 }
                 stored = true;
+            }
+        } else if constexpr (STAGE) {
+            // level 1 as below; the passing blocks go to the stage (or, when it is full, are
+            // appended by this wave at once)
+            const float sc_hi = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+            const float sc_lo = fminf(fminf(sc[0], sc[1]), fminf(sc[2], sc[3]));
+            int mrb[2];
+            bool any = false;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                int m = acc[0][nb][0];
+#pragma unroll
+                for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) m = (rb | r) ? max(m, acc[rb][nb][r]) : m;
+                mrb[nb] = m;
+                any |= ((float)m * (m >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb];
+            }
+            if (__ballot(any)) {
+                uint32_t M = 0;  // (uniform) passing blocks, bit 8 nb + rb
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
+#pragma unroll
+                    for (int rb = 0; rb < 8; ++rb) {
+                        const i32x4v_t& x = acc[rb][nb];
+                        const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
+                        if (__ballot(((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb])) M |= 1u << (8 * nb + rb);
+                    }
+                }
+                if (M) {
+                    uint32_t base = 0;
+                    if (lane == 0) {
+                        const uint32_t addr = (uint32_t)(uintptr_t)st_cnt;
+                        asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                                     : "=v"(base) : "v"(addr), "v"((uint32_t)__builtin_popcount(M)) : "memory");
+                    }
+                    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, kWave));
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                        for (int rb = 0; rb < 8; ++rb) {
+                            if (!((M >> (8 * nb + rb)) & 1u)) continue;
+                            const uint32_t slot = base + (uint32_t)__builtin_popcount(M & ((1u << (8 * nb + rb)) - 1u));
+                            const uint32_t row0 = rt * BM + rb * 16, q0 = w * 32 + nb * 16;
+                            if (slot < (uint32_t)NSTG) {
+                                *reinterpret_cast<i32x4v_t*>(st_blk + slot * 256 + lane * 4) = acc[rb][nb];
+                                if (lane == 0)
+                                    *reinterpret_cast<uint4*>(st_meta + 4 * slot) =
+                                        make_uint4(row0, q0, __float_as_uint(sc[rb >> 1]), 0u);
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r)
+                                    st_append(acc[rb][nb][r], sc[rb >> 1], row0 + 4 * (lane >> 4) + r, q0 + (lane & 15));
+                            }
+                        }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the stage is read after a barrier)
+                }
             }
         } else if constexpr (DEFER) {
             // (the epilogue runs in front of the next tile's first MFMAs, or after the loop)
@@ -984,6 +1114,23 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         if (stored) wait_vm0();  // global stores / atomics count in vmcnt: keep the waits exact
         cur_id = nxt_id;
         nxt_id = req ? __builtin_amdgcn_readfirstlane(lds_ids[t & 1]) : n2;
+    }
+    if constexpr (STAGE) {
+        // the last tile's stage, then the per-query lists to the global lists
+        __syncthreads();
+        const uint32_t n = min(*st_cnt, (uint32_t)NSTG);
+        __syncthreads();  // (everyone has read the count before it can change)
+        st_process(n);
+        __syncthreads();
+        if (tid < BN) {
+            const uint32_t c = min(st_qcnt[tid], (uint32_t)QCAP);
+            if (c) {
+                const uint32_t q = qt * BN + tid;
+                const uint32_t gp = atomicAdd(p.cnt + q, c);
+                for (uint32_t i = 0; i < c; ++i)
+                    if (gp + i < p.cap) p.cand[(uint64_t)q * p.cap + gp + i] = st_ql[tid * QCAP + i];
+            }
+        }
     }
     if constexpr (DEFER && EMIT) {  // the last tile's epilogue
         if (t > 0)
@@ -1224,7 +1371,8 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
                                                     const uint32_t* __restrict__ qflags,
                                                     uint32_t ks, float* __restrict__ tau,
                                                     uint32_t* __restrict__ cnt,
-                                                    uint32_t* __restrict__ status) {
+                                                    uint32_t* __restrict__ status,
+                                                    uint64_t* __restrict__ smax) {
     __shared__ uint64_t part[4][64 * E];
     const uint32_t q = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -1233,6 +1381,9 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
         for (uint32_t i = t; i < 8 * kTailCounters; i += blockDim.x) cnt[qpad + i] = 0;
     if (q >= qpad) return;
     if (t == 0) cnt[q] = 0;
+    // (smax, the global threshold's input: the query's ks best sample keys, or none)
+    if (smax && (q >= nq || (qflags[q] & kQueryNoApprox) || n_s < ks))
+        for (uint32_t i = t; i < ks; i += blockDim.x) smax[(uint64_t)q * ks + i] = kKeyNone;
     if (q >= nq || (qflags[q] & kQueryNoApprox)) {
         if (t == 0) tau[q] = INFINITY;  // never emits: answered by the exact scan
         return;
@@ -1297,7 +1448,34 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
 #pragma unroll
             for (int e = 0; e < E; ++e) M.offer(part[src][e * 64 + lane], (int)ks, mt);
         if (lane == 0) tau[q] = score_key_score(mt);
+        if (smax) M.store(smax + (uint64_t)q * ks, (int)ks);
     }
+}
+
+// The global emission threshold of a parallel search: tau[q] = the ks-th best
+// of the P ranks' ks best sample keys, all-gathered as g[P][qpad][ks] -- the threshold one
+// shard holding every rank's rows would select.  One wave per query.
+template <int E>
+__global__ __launch_bounds__(64) void k_global_tau(const uint64_t* __restrict__ g, uint32_t P, uint32_t qpad,
+                                                   uint32_t nq, uint32_t ks, const uint32_t* __restrict__ qflags,
+                                                   float* __restrict__ tau) {
+    const uint32_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (q >= qpad) return;
+    if (q >= nq || (qflags[q] & kQueryNoApprox)) {
+        if (lane == 0) tau[q] = INFINITY;
+        return;
+    }
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    for (uint32_t r = 0; r < P; ++r)
+        for (uint32_t b = 0; b < ks; b += kWave) {
+            const uint32_t j = b + lane;
+            L.offer(j < ks ? g[((uint64_t)r * qpad + q) * ks + j] : kKeyNone, (int)ks, thr);
+        }
+    // (fewer than ks sample keys in the whole corpus: every row is emitted)
+    if (lane == 0) tau[q] = thr == kKeyNone ? -INFINITY : score_key_score(thr);
 }
 
 // Top-(kp+1) of the emitted candidates by (score desc, row asc); the first kp go to the
@@ -1414,14 +1592,23 @@ hipError_t launch_filter_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0, h
 }
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq, uint32_t qpad,
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
-                             hipStream_t s) {
+                             hipStream_t s, uint64_t* smax) {
     if (ks > 2 * kWave) return hipErrorInvalidValue;
     if (ks > kWave)
         hipLaunchKernelGGL(k_select_tau<2>, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau,
-                           cnt, status);
+                           cnt, status, smax);
     else
         hipLaunchKernelGGL(k_select_tau<1>, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau,
-                           cnt, status);
+                           cnt, status, smax);
+    return hipGetLastError();
+}
+hipError_t launch_global_tau(const uint64_t* g, uint32_t P, uint32_t qpad, uint32_t nq, uint32_t ks,
+                             const uint32_t* qflags, float* tau, hipStream_t s) {
+    if (ks > 2 * kWave || P == 0) return hipErrorInvalidValue;
+    if (ks > kWave)
+        hipLaunchKernelGGL(k_global_tau<2>, dim3(qpad), dim3(64), 0, s, g, P, qpad, nq, ks, qflags, tau);
+    else
+        hipLaunchKernelGGL(k_global_tau<1>, dim3(qpad), dim3(64), 0, s, g, P, qpad, nq, ks, qflags, tau);
     return hipGetLastError();
 }
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,

@@ -108,9 +108,15 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 
 // tau[q] = the ks-th best sampled score (ks <= 128); also zeroes cnt[0..qpad) and the status
 // words kStFail / kStEmitted / kStFail2 for the emit pass and rescores that follow.
+// smax (optional): the query's ks best sample keys [qpad][ks] (kKeyNone where there are none),
+// the input of the global threshold of a parallel search.
 hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32_t nq,
                              uint32_t qpad, const uint32_t* qflags, uint32_t ks, float* tau,
-                             uint32_t* cnt, uint32_t* status, hipStream_t s);
+                             uint32_t* cnt, uint32_t* status, hipStream_t s, uint64_t* smax = nullptr);
+// tau[q] = the ks-th best of the all-gathered sample keys g[P][qpad][ks] (parallel search,
+// DESIGN.md §6); INFINITY for padding / no-filter queries.
+hipError_t launch_global_tau(const uint64_t* g, uint32_t P, uint32_t qpad, uint32_t nq, uint32_t ks,
+                             const uint32_t* qflags, float* tau, hipStream_t s);
 // The k' = kp best emitted candidates (rows) and tau_excl = the (kp+1)-th score, for lists
 // larger than kFusedSelectCap (smaller ones are selected inside the rescore).
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap,
@@ -163,6 +169,12 @@ struct RescoreArgs {
     const uint32_t* emit_cnt;
     uint32_t* cur_status;
     uint32_t n_queries;
+    // Parallel search with a global threshold (mode B, one wave per query): no
+    // local certification -- every query's list of its rescored emitted rows becomes its
+    // result (count = min(k, rows rescored)) and excl_out[q] receives the distance below which
+    // no row left out can lie (1 - tau0 - E_q - 2.5e-7 rounded down; -inf when nothing can be
+    // certified, +inf when every row was a candidate); the root certifies the merged lists.
+    float* excl_out;
 };
 // Workgroups of the device-counted rescore (failed certifications, usually a few queries).
 constexpr uint32_t kRescoreAllGrid = 128;
@@ -184,6 +196,32 @@ constexpr uint32_t kMergeMaxEntries = 1024;
 hipError_t launch_merge_lists(const uint64_t* idx, const float* dist, const uint32_t* cnt, uint32_t P, uint32_t nq,
                               uint32_t k_in, uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count,
                               uint32_t* first_nan, hipStream_t s);
+// The general form: strided lists (the all-gathered packed result buffers of a parallel search)
+// and, with excl, the certification of a global-threshold search.
+struct MergeArgs {
+    const uint64_t* idx;        // list l of query q: idx + l * idx_stride + q * k_in
+    const float* dist;          // dist + l * dist_stride + q * k_in
+    const uint32_t* cnt;        // cnt[l * cnt_stride + q]
+    uint64_t idx_stride, dist_stride, cnt_stride;
+    uint32_t P, nq, k_in, k;
+    uint64_t* out_idx;          // [nq][k]
+    float* out_dist;
+    uint32_t* out_count;        // [nq]
+    uint32_t* first_nan;        // ~0 before the launch
+    // certification (optional): list l's exclusion bounds excl[l * excl_stride + q]; a query
+    // is certified iff its merged list holds need = min(k, corpus rows) entries and the k-th
+    // distance is below every bound -- the others are appended to fail_list / *fail_cnt
+    const float* excl;
+    uint64_t excl_stride;
+    uint32_t need;
+    uint32_t* fail_cnt;
+    uint32_t* fail_list;
+    // (optional) each list's kStWords status words, st[l * st_stride + w] -> st_all[l][w]
+    const uint32_t* st;
+    uint64_t st_stride;
+    uint32_t* st_all;
+};
+hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
 // Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
 // result buffer the next search will use.
 // status: the NEXT search's status words (zeroed); emit_cnt (optional): per-query emitted

@@ -8,8 +8,11 @@ offset), then calls bsr_parallel_top_k_similarity_search on the whole query batc
   fail_last  the last rank's index has max_k < k, so its GPU search fails;
   fail_root  the same on rank 0;
   shape      the last rank passes one query fewer (collective rejection);
-  hook_fault the last rank's header all-gather, issued from the search's hook, fails before it
-             is posted (BSR_INJECT_FAULT): the rank must still post it, with its error status.
+  hook_fault the last rank's header all-gather fails before it is posted (BSR_INJECT_FAULT):
+             the rank must still post it, with its error status;
+  gtau_fallback  no merged list of the global-threshold search certifies (BSR_INJECT_FAULT):
+             every query takes the collective fallback (the standard parallel search);
+  no_gtau    the global threshold turned off (BSR_GLOBAL_TAU=0): the standard parallel search.
 The rank writes {status, message, and on the root the lists} to <out>.rank<r>.npz.
 """
 import argparse
@@ -47,6 +50,10 @@ def main():
     os.environ["MASTER_PORT"] = str(a.port)
     if a.case == "hook_fault":
         os.environ["BSR_INJECT_FAULT"] = f"header_hook:{a.world - 1}"
+    if a.case == "gtau_fallback":
+        os.environ["BSR_INJECT_FAULT"] = "gtau_uncertified"
+    if a.case == "no_gtau":
+        os.environ["BSR_GLOBAL_TAU"] = "0"
     import torch  # noqa: F401  (before libbsr: one HIP runtime per process, tests/conftest.py)
     import torch.distributed as dist
     import bsr
@@ -71,14 +78,15 @@ def main():
             status, msg = e.status, str(e)
         warned = [str(x.message) for x in w]
     dist.barrier()
+    st = ix.last_stats()
     out = {"status": np.int32(status), "msg": np.frombuffer(msg.encode() or b" ", np.uint8),
+           "emitted": np.uint64(st.n_emitted), "fallback": np.uint32(st.n_fallback),
            "warned": np.frombuffer(("|".join(warned) or " ").encode(), np.uint8)}
     if res is not None:
         out.update(idx=res[0], dist=res[1], cnt=res[2])
     if a.rank == 0 or res is None:
         out["is_none"] = np.int32(res is None)
     np.savez(f"{a.out}.rank{a.rank}.npz", **out)
-    st = ix.last_stats()
     print(f"rank {a.rank}: status {status} graph_replay {st.graph_replay} emitted {st.n_emitted}", flush=True)
     comm.close()
     ix.close()

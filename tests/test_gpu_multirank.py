@@ -74,10 +74,15 @@ def _same(r, want):
         assert np.array_equal(r["dist"][q, :c].view(np.uint32), wd[q, :c].view(np.uint32)), q
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_parallel_search_multirank_matches_oracle(bsr_mod, oracle_mod, gpu, corpus, tmp_path, world):
+@pytest.mark.parametrize("world,case", [(2, "normal"), (3, "normal"), (8, "normal"), (3, "no_gtau"),
+                                        (3, "gtau_fallback")])
+def test_parallel_search_multirank_matches_oracle(bsr_mod, oracle_mod, gpu, corpus, tmp_path, world, case):
+    """normal: the global-threshold search (every rank emits against the threshold selected from
+    every rank's sample, rescores all it emitted; the merged lists certified); no_gtau: the
+    standard path (local certified searches); gtau_fallback: every merged list uncertified, so
+    every query takes the collective fallback -- all bit-exact against the oracle."""
     rows, q = corpus
-    res = _run(world, "normal", tmp_path)
+    res = _run(world, case, tmp_path)
     for r in range(world):
         assert int(res[r]["status"]) == 0, res[r]["msg"].tobytes()
     for r in range(1, world):
@@ -86,6 +91,14 @@ def test_parallel_search_multirank_matches_oracle(bsr_mod, oracle_mod, gpu, corp
     # self-matches: the planted rows come first at distance 0
     assert [int(res[0]["idx"][i, 0]) for i in range(3)] == [0, mr_worker.N // 2 + 3, mr_worker.N - 1]
     assert not res[0]["dist"][:3, 0].any()
+    nq = len(q)
+    if case == "normal":
+        # the global threshold: ~256 rows per query over the whole corpus, not per rank
+        total = sum(int(res[r]["emitted"]) for r in range(world))
+        assert total / nq < 600, total / nq
+        assert int(res[0]["fallback"]) == 0
+    if case == "gtau_fallback":
+        assert int(res[0]["fallback"]) == nq
 
 
 def test_parallel_search_failing_rank(bsr_mod, oracle_mod, gpu, corpus, tmp_path):

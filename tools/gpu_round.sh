@@ -11,7 +11,8 @@
 #   pmc         HBM traffic (FETCH_SIZE, WRITE_SIZE) at 10M / 5M / 2.5M / 1.25M rows into a copy of
 #               profiles/pmc_traffic.json, then one SQ/GRBM pass at 10M
 #   pmcsmall    two SQ passes (issue, LDS, waits) over the default bench
-#   rehearsal   --gpus 2 and 4 over the host transport on the one GPU (spawn, exchange, root merge)
+#   rehearsal   --gpus 2, 4 and 8 over the host transport on the one GPU (spawn, exchange, root merge)
+#   mr          the multi-rank GPU tests alone (tests/test_gpu_multirank.py)
 #   stamps      s_memtime phase split of the emit filter (make lab-fstamps) at 10M and 1.25M
 #   counters    emission-epilogue event counts + per-workgroup balance (make lab-counters)
 #   fab         tools/microbench/filter_ab (product vs variants of the emit filter) at 10M and 1.25M
@@ -83,11 +84,14 @@ for step in $STEPS; do
           SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE --output-format csv -d "$O/ps/p2" -o run -- $B
       python3 tools/microbench/pmc_summary.py "$O/ps" > "$O/pmc_small_summary.txt" ;;
     rehearsal)
-      for n in 2 4; do
+      for n in 2 4 8; do
         run 400 "bench N=$n host" "$O/bench_n$n.json" python bench.py --gpus $n --comm host --steps 10 --warmup 2 --verify 2 \
             --no-cpu-baseline
         head -c 600 "$O/bench_n$n.json"; echo
       done ;;
+    mr)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 200 --timeout-method thread > "$O/pytest_mr.log" 2>&1
+      rc=$?; echo "pytest mr rc=$rc"; tail -12 "$O/pytest_mr.log"; [ $rc -eq 0 ] || exit $rc ;;
     stamps)
       for rows in 10000000 1250000; do
         BSR_LIB=tools/ab/libbsr_fstamps.so run 240 "stamps $rows" "$O/stamps_$rows.txt" python tools/diag/filter_stamps.py $rows

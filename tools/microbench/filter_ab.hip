@@ -63,13 +63,12 @@ int main(int argc, char** argv) {
 
     struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; };
     std::vector<V> vs = {
-        {"product", bsr::k_filter_qs16<true, 12, false, 0>, {}},
-        {"tailx8", bsr::k_filter_qs16<true, 12, false, 8>, {}},
-        {"tailx2", bsr::k_filter_qs16<true, 12, false, 2>, {}},
-        {"tailx1", bsr::k_filter_qs16<true, 12, false, 1>, {}},
-        {"defer+tailx8", bsr::k_filter_qs16<true, 12, true, 8>, {}},
-        {"defer+tailx1", bsr::k_filter_qs16<true, 12, true, 1>, {}},
+        {"tailx0", bsr::k_filter_qs16<true, 12, 0, 0>, {}},
+        {"product", bsr::k_filter_qs16<true, 12, 0, 8>, {}},
+        {"stage", bsr::k_filter_qs16<true, 12, 2, 8>, {}},
+        {"defer", bsr::k_filter_qs16<true, 12, 1, 8>, {}},
     };
+
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
