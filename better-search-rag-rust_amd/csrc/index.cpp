@@ -799,6 +799,7 @@ int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
         qsrc = q_in.as<float>();
     }
+    ev_begin(ix, ev_total);
     QueryPrepArgs qa{};
     qa.q = qsrc;
     qa.nq = nq;
@@ -860,6 +861,7 @@ int bsr_index::gtau_phase_b(const uint64_t* g_smax, uint32_t P) {
     ra.n_queries = nq;
     BSR_HIP(launch_rescore(ra, stream));
     ev_end(ix, ev_rescore);
+    ev_end(ix, ev_total);  // (the local part: phases A and B, the all-gather between them included)
     next_status_clean = true;
     return BSR_OK;
 }

@@ -1454,13 +1454,13 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
 
 // The global emission threshold of a parallel search: tau[q] = the ks-th best
 // of the P ranks' ks best sample keys, all-gathered as g[P][qpad][ks] -- the threshold one
-// shard holding every rank's rows would select.  One wave per query.
+// shard holding every rank's rows would select.  One wave per query, four per workgroup.
 template <int E>
-__global__ __launch_bounds__(64) void k_global_tau(const uint64_t* __restrict__ g, uint32_t P, uint32_t qpad,
-                                                   uint32_t nq, uint32_t ks, const uint32_t* __restrict__ qflags,
-                                                   float* __restrict__ tau) {
-    const uint32_t q = blockIdx.x;
-    const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) void k_global_tau(const uint64_t* __restrict__ g, uint32_t P, uint32_t qpad,
+                                                    uint32_t nq, uint32_t ks, const uint32_t* __restrict__ qflags,
+                                                    float* __restrict__ tau) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (q >= qpad) return;
     if (q >= nq || (qflags[q] & kQueryNoApprox)) {
         if (lane == 0) tau[q] = INFINITY;
@@ -1606,9 +1606,9 @@ hipError_t launch_global_tau(const uint64_t* g, uint32_t P, uint32_t qpad, uint3
                              const uint32_t* qflags, float* tau, hipStream_t s) {
     if (ks > 2 * kWave || P == 0) return hipErrorInvalidValue;
     if (ks > kWave)
-        hipLaunchKernelGGL(k_global_tau<2>, dim3(qpad), dim3(64), 0, s, g, P, qpad, nq, ks, qflags, tau);
+        hipLaunchKernelGGL(k_global_tau<2>, dim3(qpad / 4), dim3(256), 0, s, g, P, qpad, nq, ks, qflags, tau);
     else
-        hipLaunchKernelGGL(k_global_tau<1>, dim3(qpad), dim3(64), 0, s, g, P, qpad, nq, ks, qflags, tau);
+        hipLaunchKernelGGL(k_global_tau<1>, dim3(qpad / 4), dim3(256), 0, s, g, P, qpad, nq, ks, qflags, tau);
     return hipGetLastError();
 }
 hipError_t launch_select_cand(const uint64_t* cand, const uint32_t* cnt, uint32_t cap, uint32_t nq,

@@ -13,9 +13,12 @@
 #   pmcsmall    two SQ passes (issue, LDS, waits) over the default bench
 #   rehearsal   --gpus 2, 4 and 8 over the host transport on the one GPU (spawn, exchange, root merge)
 #   mr          the multi-rank GPU tests alone (tests/test_gpu_multirank.py)
+#   rehprof     rocprofv3 kernel stats of the --gpus 8 host rehearsal (every rank process traced)
 #   stamps      s_memtime phase split of the emit filter (make lab-fstamps) at 10M and 1.25M
 #   counters    emission-epilogue event counts + per-workgroup balance (make lab-counters)
 #   fab         tools/microbench/filter_ab (product vs variants of the emit filter) at 10M and 1.25M
+#   fabshard    filter_ab at the rank shards of N = 2, 4, 8 (5M, 2.5M, 1.25M rows) at the global threshold's
+#               emission rate (tau 0.1473: ~256 rows per query over the 10M corpus, 256/N per rank)
 #   fabpmc      FETCH_SIZE of each filter_ab variant at 10M and 1.25M (HBM traffic per launch)
 #   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
 #               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard
@@ -89,6 +92,11 @@ for step in $STEPS; do
             --no-cpu-baseline
         head -c 600 "$O/bench_n$n.json"; echo
       done ;;
+    rehprof)
+      run 600 "rehearsal N=8 rocprof" "$O/bench_n8_prof.json" rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$O/rehprof" -o run -- python3 bench.py --gpus 8 --comm host --steps 10 --warmup 2 --verify 0 --no-cpu-baseline \
+          --p50-iters 3
+      find "$O/rehprof" -name "*kernel_stats.csv" | head -3 ;;
     mr)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 200 --timeout-method thread > "$O/pytest_mr.log" 2>&1
       rc=$?; echo "pytest mr rc=$rc"; tail -12 "$O/pytest_mr.log"; [ $rc -eq 0 ] || exit $rc ;;
@@ -107,6 +115,11 @@ for step in $STEPS; do
     fab)
       run 300 "filter_ab 10M" "$O/fab_10m.txt" tools/microbench/filter_ab 10000000 1000 10 0.1473; cat "$O/fab_10m.txt"
       run 200 "filter_ab 1.25M" "$O/fab_125.txt" tools/microbench/filter_ab 1250000 1000 30 0.1284; cat "$O/fab_125.txt" ;;
+    fabshard)
+      for rows in 5000000 2500000 1250000; do
+        run 300 "filter_ab $rows" "$O/fab_$rows.txt" tools/microbench/filter_ab $rows 1000 20 0.1473
+        grep -E "emitted|median" "$O/fab_$rows.txt"
+      done ;;
     fabpmc)
       for rows in 10000000 1250000; do
         run 300 "filter_ab pmc $rows" /dev/null rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fabpmc_$rows" -o run -- \
