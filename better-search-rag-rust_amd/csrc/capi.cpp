@@ -99,8 +99,17 @@ struct bsr_comm {
     bool hdr_posted = false;       // this search's header all-gather has been issued
     // the global-threshold search (parallel_gtau): gathered sample keys, gathered result
     // buffers, the merged result (device and pinned host), the fallback queries
-    DevBuf g_smax, g_res, m_res, fb_q;
-    PinnedVec<uint8_t> h_mres, h_stage;
+    DevBuf g_smax, g_res, m_res, fb_q, pub_ticket;
+    PinnedVec<uint8_t> h_stage;
+    uint8_t* h_mres = nullptr;      // fine-grained pinned: the merge kernel publishes into it
+    uint8_t* h_mres_dev = nullptr;
+    size_t h_mres_bytes = 0;
+    uint32_t* h_flag = nullptr;     // fine-grained host word the merge kernel raises
+    uint32_t* h_flag_dev = nullptr;
+    ~bsr_comm() {
+        if (h_mres) (void)hipHostFree(h_mres);
+        if (h_flag) (void)hipHostFree(h_flag);
+    }
 };
 
 // The parallel search's header, all-gathered before the lists: every rank's batch shape
@@ -656,9 +665,23 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     const size_t nqk = (size_t)nq * k;
     const size_t o_st = 16, o_fail = round_up(o_st + (size_t)P * kStWords * 4, 16),
                  o_cnt = round_up(o_fail + (size_t)nq * 4, 16), o_dist = round_up(o_cnt + (size_t)nq * 4, 16),
-                 o_idx = round_up(o_dist + nqk * 4, 16), mbytes = o_idx + nqk * 8;
+                 o_idx = round_up(o_dist + nqk * 4, 16), mbytes = round_up(o_idx + nqk * 8, 16);
     BSR_TRY(c->m_res.ensure(mbytes));
-    BSR_TRY(c->h_mres.resize(mbytes));
+    if (c->h_mres_bytes < mbytes) {
+        if (c->h_mres) BSR_HIP(hipHostFree(c->h_mres));
+        c->h_mres = nullptr;
+        c->h_mres_bytes = 0;
+        BSR_HIP(hipHostMalloc((void**)&c->h_mres, mbytes, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_mres_dev, c->h_mres, 0));
+        c->h_mres_bytes = mbytes;
+    }
+    if (!c->h_flag) {
+        BSR_HIP(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_flag_dev, c->h_flag, 0));
+        BSR_TRY(c->pub_ticket.ensure(sizeof(uint32_t)));
+        BSR_HIP(hipMemsetAsync(c->pub_ticket.p, 0, sizeof(uint32_t), s));
+    }
+    __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
     uint8_t* md = c->m_res.as<uint8_t>();
     BSR_HIP(hipMemsetAsync(md, 0, 4, s));         // fail count
     BSR_HIP(hipMemsetAsync(md + 4, 0xff, 4, s));  // the lowest query with a NaN distance: none
@@ -686,10 +709,20 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     ma.st = reinterpret_cast<const uint32_t*>(g);
     ma.st_stride = rbytes / 4;
     ma.st_all = reinterpret_cast<uint32_t*>(md + o_st);
+    // the merge publishes its result into host memory and raises the flag (no D2H copy, no
+    // wait for the completion signal: index.cpp flag_wait)
+    ma.pub_src = md;
+    ma.pub_dst = c->h_mres_dev;
+    ma.pub_bytes = mbytes;
+    ma.pub_flag = c->h_flag_dev;
+    ma.pub_ticket = c->pub_ticket.as<uint32_t>();
     BSR_HIP(launch_merge(ma, s));
-    uint8_t* hm = c->h_mres.data();
-    BSR_HIP(hipMemcpyAsync(hm, md, mbytes, hipMemcpyDeviceToHost, s));
-    BSR_HIP(stream_wait(s));
+    uint8_t* hm = c->h_mres;
+    {
+        const hipError_t r = flag_wait(c->h_flag, s);
+        if (r == hipErrorUnknown) return set_error(BSR_E_HIP, "the merge finished without publishing its result");
+        BSR_HIP(r);
+    }
     bsr_index_collect_profile_impl(ix);
     const uint32_t* hw = reinterpret_cast<const uint32_t*>(hm);
     const uint32_t* st_all = reinterpret_cast<const uint32_t*>(hm + o_st);

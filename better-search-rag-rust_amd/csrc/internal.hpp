@@ -48,6 +48,9 @@ struct DevBuf {
 
 bool is_device_ptr(const void* p);
 hipError_t stream_wait(hipStream_t s);  // poll until the stream's work is done
+// Poll a host flag a publishing kernel raises (checking the stream now and then): hipSuccess,
+// the stream's error, or hipErrorUnknown when the stream finished without raising it.
+hipError_t flag_wait(const uint32_t* flag, hipStream_t s);
 int select_device(int device);
 
 static inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
@@ -89,8 +92,12 @@ struct bsr_index {
     // indices].  One D2H copy per search reads it all back (into pinned memory); the
     // finalize kernel of search i zeroes the status words of the buffer search i+1 uses.
     bsr::DevBuf res[2];
-    uint8_t* h_res = nullptr;  // pinned (hipHostMalloc) mirror of one result buffer
+    uint8_t* h_res = nullptr;  // pinned, fine-grained (hipHostMallocCoherent) mirror of one result buffer
+    uint8_t* h_res_dev = nullptr;   // its device-side address (the publishing kernel writes it)
     size_t h_res_bytes = 0;
+    uint32_t* h_flag = nullptr;     // fine-grained host word raised by the publishing kernel
+    uint32_t* h_flag_dev = nullptr;
+    bsr::DevBuf pub_ticket;         // device word: workgroups finished in the publishing kernel
     uint32_t cur = 0;          // result buffer of the last search
     bool next_status_clean = false;  // status words of res[cur ^ 1] are known to be zero
     size_t res_off_cnt = 0, res_off_dist = 0, res_off_idx = 0, res_off_x = 0, res_bytes = 0;

@@ -397,6 +397,29 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         }
         BSR_STAMP(W, 4);
     }
+    if (a.pub_flag) {
+        // publish: every workgroup's writes released (agent scope) before its ticket; the last
+        // one acquires them, copies the packed result to host memory, releases it at system
+        // scope and raises the flag the host polls
+        __shared__ uint32_t s_last;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            const size_t n16 = a.pub_bytes / 16;
+            const uint4* src = reinterpret_cast<const uint4*>(a.pub_src);
+            uint4* dst = reinterpret_cast<uint4*>(a.pub_dst);
+            for (size_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+            __threadfence_system();
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                *a.pub_ticket = 0u;
+                __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -614,131 +637,157 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
-    if (a.st_all && q == 0)  // every list's status words, compact
-        for (uint32_t i = lane; i < P * kStWords; i += kWave)
-            a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
-    if (q >= nq) return;
-    // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
-    const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
-    uint32_t incl = c_l;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)incl, off, kWave);
-        if (lane >= off) incl += t;
-    }
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t off_l = incl - c_l;
-    bool nan = false;
-    for (uint32_t l = 0; l < P; ++l) {
-        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, (int)l);
-        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)l);
-        const uint64_t bi = (uint64_t)l * a.idx_stride + (uint64_t)q * k_in;
-        const uint64_t bd = (uint64_t)l * a.dist_stride + (uint64_t)q * k_in;
-        for (uint32_t i = lane; i < c; i += kWave) {
-            const float d = dist[bd + i];
-            nan |= d != d;
-            s_idx[o + i] = idx[bi + i];
-            s_dist[o + i] = d;
-            s_key[o + i] = ((uint64_t)ord_f32(d + 0.0f) << 32) | (o + i);  // (-0.0 + 0.0 = +0.0)
+    auto merge_query = [&]() {
+        if (a.st_all && q == 0)  // every list's status words, compact
+            for (uint32_t i = lane; i < P * kStWords; i += kWave)
+                a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
+        if (q >= nq) return;
+        // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
+        const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
+        uint32_t incl = c_l;
+    #pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, off, kWave);
+            if (lane >= off) incl += t;
         }
-    }
-    __syncthreads();
-    uint64_t* const oi = out_idx + (uint64_t)q * k;
-    float* const od = out_dist + (uint64_t)q * k;
-    if (__ballot(nan)) {
-        if (lane == 0) {
-            out_count[q] = 0;
-            atomicMin(a.first_nan, q);
-        }
-        for (uint32_t p = lane; p < k; p += kWave) {
-            oi[p] = ~0ull;
-            od[p] = INFINITY;
-        }
-        return;
-    }
-    // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
-    // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
-    // hash's empty mark, takes the pairwise check instead.)
-    bool has_empty_mark = false;
-    for (uint32_t j = lane; j < total; j += kWave) has_empty_mark |= s_idx[j] == ~0ull;
-    const bool pairwise = __ballot(has_empty_mark) != 0;
-    uint32_t hmask = 127;
-    while (hmask + 1 < 2 * total && hmask + 1 < kMergeMaxEntries) hmask = 2 * hmask + 1;  // load <= 1
-    auto slot0 = [&](uint64_t x) -> uint32_t {
-        uint64_t h = x * 0x9E3779B97F4A7C15ull;
-        return (uint32_t)(h >> 40) & hmask;
-    };
-    if (!pairwise) {
-        for (uint32_t i = lane; i <= hmask; i += kWave) {
-            h_idx[i] = ~0ull;
-            h_min[i] = ~0ull;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t off_l = incl - c_l;
+        bool nan = false;
+        for (uint32_t l = 0; l < P; ++l) {
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, (int)l);
+            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)l);
+            const uint64_t bi = (uint64_t)l * a.idx_stride + (uint64_t)q * k_in;
+            const uint64_t bd = (uint64_t)l * a.dist_stride + (uint64_t)q * k_in;
+            for (uint32_t i = lane; i < c; i += kWave) {
+                const float d = dist[bd + i];
+                nan |= d != d;
+                s_idx[o + i] = idx[bi + i];
+                s_dist[o + i] = d;
+                s_key[o + i] = ((uint64_t)ord_f32(d + 0.0f) << 32) | (o + i);  // (-0.0 + 0.0 = +0.0)
+            }
         }
         __syncthreads();
-        for (uint32_t j = lane; j < total; j += kWave) {
-            const uint64_t x = s_idx[j];
-            for (uint32_t sl = slot0(x);; sl = (sl + 1) & hmask) {
-                const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&h_idx[sl]), ~0ull,
-                                                (unsigned long long)x);
-                if (prev == ~0ull || prev == x) {
-                    atomicMin(reinterpret_cast<unsigned long long*>(&h_min[sl]), (unsigned long long)s_key[j]);
-                    break;
+        uint64_t* const oi = out_idx + (uint64_t)q * k;
+        float* const od = out_dist + (uint64_t)q * k;
+        if (__ballot(nan)) {
+            if (lane == 0) {
+                out_count[q] = 0;
+                atomicMin(a.first_nan, q);
+            }
+            for (uint32_t p = lane; p < k; p += kWave) {
+                oi[p] = ~0ull;
+                od[p] = INFINITY;
+            }
+            return;
+        }
+        // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
+        // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
+        // hash's empty mark, takes the pairwise check instead.)
+        bool has_empty_mark = false;
+        for (uint32_t j = lane; j < total; j += kWave) has_empty_mark |= s_idx[j] == ~0ull;
+        const bool pairwise = __ballot(has_empty_mark) != 0;
+        uint32_t hmask = 127;
+        while (hmask + 1 < 2 * total && hmask + 1 < kMergeMaxEntries) hmask = 2 * hmask + 1;  // load <= 1
+        auto slot0 = [&](uint64_t x) -> uint32_t {
+            uint64_t h = x * 0x9E3779B97F4A7C15ull;
+            return (uint32_t)(h >> 40) & hmask;
+        };
+        if (!pairwise) {
+            for (uint32_t i = lane; i <= hmask; i += kWave) {
+                h_idx[i] = ~0ull;
+                h_min[i] = ~0ull;
+            }
+            __syncthreads();
+            for (uint32_t j = lane; j < total; j += kWave) {
+                const uint64_t x = s_idx[j];
+                for (uint32_t sl = slot0(x);; sl = (sl + 1) & hmask) {
+                    const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&h_idx[sl]), ~0ull,
+                                                    (unsigned long long)x);
+                    if (prev == ~0ull || prev == x) {
+                        atomicMin(reinterpret_cast<unsigned long long*>(&h_min[sl]), (unsigned long long)s_key[j]);
+                        break;
+                    }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
-    }
-    WaveTopK<E> L;
-    L.init();
-    uint64_t thr = kKeyNone;
-    for (uint32_t b = 0; b < total; b += kWave) {
-        const uint32_t j = b + lane;
-        uint64_t key = kKeyNone;
-        if (j < total) {
-            key = s_key[j];
-            const uint64_t x = s_idx[j];
-            if (!pairwise) {
-                uint32_t sl = slot0(x);
-                while (h_idx[sl] != x) sl = (sl + 1) & hmask;
-                if (h_min[sl] != key) key = kKeyNone;
-            } else {
-                for (uint32_t i = 0; i < total; ++i)  // an earlier-sorting copy of the same index
-                    if (s_idx[i] == x && s_key[i] < key) { key = kKeyNone; break; }
+        WaveTopK<E> L;
+        L.init();
+        uint64_t thr = kKeyNone;
+        for (uint32_t b = 0; b < total; b += kWave) {
+            const uint32_t j = b + lane;
+            uint64_t key = kKeyNone;
+            if (j < total) {
+                key = s_key[j];
+                const uint64_t x = s_idx[j];
+                if (!pairwise) {
+                    uint32_t sl = slot0(x);
+                    while (h_idx[sl] != x) sl = (sl + 1) & hmask;
+                    if (h_min[sl] != key) key = kKeyNone;
+                } else {
+                    for (uint32_t i = 0; i < total; ++i)  // an earlier-sorting copy of the same index
+                        if (s_idx[i] == x && s_key[i] < key) { key = kKeyNone; break; }
+                }
+            }
+            L.offer(key, (int)k, thr);
+        }
+        uint32_t got = 0;
+    #pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t p = e * kWave + lane;
+            const uint64_t key = L.v[e];
+            got += (uint32_t)__popcll(__ballot(p < k && key != kKeyNone));
+            if (p < k) {
+                const uint32_t j = (uint32_t)key;
+                oi[p] = key != kKeyNone ? s_idx[j] : ~0ull;
+                od[p] = key != kKeyNone ? s_dist[j] : INFINITY;
             }
         }
-        L.offer(key, (int)k, thr);
-    }
-    uint32_t got = 0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t p = e * kWave + lane;
-        const uint64_t key = L.v[e];
-        got += (uint32_t)__popcll(__ballot(p < k && key != kKeyNone));
-        if (p < k) {
-            const uint32_t j = (uint32_t)key;
-            oi[p] = key != kKeyNone ? s_idx[j] : ~0ull;
-            od[p] = key != kKeyNone ? s_dist[j] : INFINITY;
+        if (lane == 0) out_count[q] = got;
+        const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
+        if (a.excl && lane == 0) {
+            // Certification of a global-threshold parallel search: every row left
+            // out on rank l lies at a distance >= excl_l[q] (its kernel's bound, rounded down), so
+            // the merged list is the reference's iff it holds need = min(k, corpus rows) entries and
+            // its k-th distance lies strictly below every rank's bound (a shorter list only when
+            // every row of the corpus was a candidate: every bound +inf).
+            float xmin = INFINITY;
+            for (uint32_t l = 0; l < P; ++l) {
+                const float x = a.excl[(uint64_t)l * a.excl_stride + q];
+                xmin = x == x ? fminf(xmin, x) : -INFINITY;
+            }
+            bool ok = got >= a.need;
+            if (ok && got == k) {
+                ok = (double)s_dist[(uint32_t)kth] < (double)xmin;
+            } else if (ok) {
+                ok = xmin == INFINITY;
+            }
+            if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
         }
-    }
-    if (lane == 0) out_count[q] = got;
-    const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
-    if (a.excl && lane == 0) {
-        // Certification of a global-threshold parallel search: every row left
-        // out on rank l lies at a distance >= excl_l[q] (its kernel's bound, rounded down), so
-        // the merged list is the reference's iff it holds need = min(k, corpus rows) entries and
-        // its k-th distance lies strictly below every rank's bound (a shorter list only when
-        // every row of the corpus was a candidate: every bound +inf).
-        float xmin = INFINITY;
-        for (uint32_t l = 0; l < P; ++l) {
-            const float x = a.excl[(uint64_t)l * a.excl_stride + q];
-            xmin = x == x ? fminf(xmin, x) : -INFINITY;
+
+    };
+    merge_query();
+    if (a.pub_flag) {
+        // publish (as k_rescore's): the last workgroup copies the merged result to host memory
+        // and raises the host's flag
+        __shared__ uint32_t s_last;
+        __threadfence();
+        __syncthreads();
+        if (lane == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            const size_t n16 = a.pub_bytes / 16;
+            const uint4* src = reinterpret_cast<const uint4*>(a.pub_src);
+            uint4* dst = reinterpret_cast<uint4*>(a.pub_dst);
+            for (size_t i = lane; i < n16; i += kWave) dst[i] = src[i];
+            __threadfence_system();
+            __syncthreads();
+            if (lane == 0) {
+                *a.pub_ticket = 0u;
+                __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
-        bool ok = got >= a.need;
-        if (ok && got == k) {
-            ok = (double)s_dist[(uint32_t)kth] < (double)xmin;
-        } else if (ok) {
-            ok = xmin == INFINITY;
-        }
-        if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
     }
 }
 

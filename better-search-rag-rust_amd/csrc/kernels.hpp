@@ -175,6 +175,15 @@ struct RescoreArgs {
     // no row left out can lie (1 - tau0 - E_q - 2.5e-7 rounded down; -inf when nothing can be
     // certified, +inf when every row was a candidate); the root certifies the merged lists.
     float* excl_out;
+    // Publish (optional, the batch's last kernel): the workgroup that finishes last copies
+    // pub_bytes of the packed result buffer pub_src to host memory pub_dst (fine-grained pinned)
+    // and then sets *pub_flag = 1 with a system-scope release, so the host sees the result
+    // without waiting for the stream's completion signal and without a D2H copy node.
+    const uint8_t* pub_src;
+    uint8_t* pub_dst;
+    size_t pub_bytes;
+    uint32_t* pub_flag;
+    uint32_t* pub_ticket;       // device word, 0 between launches
 };
 // Workgroups of the device-counted rescore (failed certifications, usually a few queries).
 constexpr uint32_t kRescoreAllGrid = 128;
@@ -220,6 +229,12 @@ struct MergeArgs {
     const uint32_t* st;
     uint64_t st_stride;
     uint32_t* st_all;
+    // (optional) publish the merged result buffer to host memory, as RescoreArgs::pub_*
+    const uint8_t* pub_src;
+    uint8_t* pub_dst;
+    size_t pub_bytes;
+    uint32_t* pub_flag;
+    uint32_t* pub_ticket;
 };
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
 // Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
