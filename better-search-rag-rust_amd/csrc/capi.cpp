@@ -810,6 +810,7 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     else if (c && !c->host_fn && c->device != ix->device)
         st = set_error(BSR_E_INVALID, "communicator and index on different devices");
     const bool multi = c && c->size > 1;
+    bool searched = false;
     if (multi) {
         // global threshold: this rank's filter path with a sample pass, lists the device merge
         // takes, and the library setting (BSR_GLOBAL_TAU=0 turns it off)
@@ -817,7 +818,9 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
             const char* v = getenv("BSR_GLOBAL_TAU");
             return !(v && v[0] == '0');
         }();
-        bool gt = allow_gtau && gtau_on && st == BSR_OK && ix->gtau_eligible(nq, k) &&
+        // (batches of <= 16 queries -- the latency path -- keep the per-rank threshold: their
+        // emission is light, and the standard path overlaps the header with the search)
+        bool gt = allow_gtau && gtau_on && st == BSR_OK && nq > kSkinnyMaxQ && ix->gtau_eligible(nq, k) &&
                   device_merge_fits((uint32_t)c->size, k, k);
         if (gt) {
             const int r = ix->gtau_phase_a(queries, nq, k);  // (enqueued: the header overlaps it)
@@ -831,7 +834,23 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
             gt = false;
             BSR_TRY(header_start(c, nq, k, st, false, ix ? ix->n : 0));
         }
-        BSR_TRY(header_wait(c));
+        if (!gt) {
+            // this rank is not on the global-threshold path, so no rank is: its standard search
+            // starts now, and the header's wait rides the search's hook (overlapping the search)
+            struct HookCtx { bsr_comm* c; int st; bool ran; } hc{c, BSR_OK, false};
+            auto hook = [](void* p) -> int {
+                HookCtx* h = static_cast<HookCtx*>(p);
+                h->ran = true;
+                h->st = header_wait(h->c);
+                return h->st;
+            };
+            if (st == BSR_OK) st = ix->search_device(queries, nq, k, +hook, &hc);
+            if (!hc.ran) hc.st = header_wait(c);  // (the search failed before its launch, or never ran)
+            if (hc.st != BSR_OK) return hc.st;   // (a transport error: every rank sees it)
+            searched = true;
+        } else {
+            BSR_TRY(header_wait(c));
+        }
         const int32_t* h0 = header_of(c, 0);
         bool all_gt = true;
         for (int32_t r = 0; r < c->size; ++r) {
@@ -843,11 +862,11 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
                                  h0[0], h0[1], r, hr[0], hr[1]);
             all_gt &= hr[4] == 1 && hr[2] == BSR_OK;
         }
-        if (all_gt) return parallel_gtau(c, ix, queries, nq, k, out_idx, out_dist, out_count);
+        if (gt && all_gt) return parallel_gtau(c, ix, queries, nq, k, out_idx, out_dist, out_count);
         if (gt) BSR_HIP(stream_wait(ix->stream));  // (phase A ran for nothing: the standard path)
     }
     // compute_local_top_k (:185-191)
-    if (st == BSR_OK) st = ix->search_device(queries, nq, k);
+    if (st == BSR_OK && !searched) st = ix->search_device(queries, nq, k);
     if (!c) {  // one rank, no communicator: the local lists are the result
         BSR_TRY(st);
         if (!nq) return BSR_OK;
