@@ -644,7 +644,9 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     if (nq == 0) return BSR_OK;
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
 
-    const uint32_t qpad = (uint32_t)round_up(nq, kFilterTile);
+    // queries padded to the filter's 256-query tile; batches of <= 16 (the skinny kernels read
+    // query rows 0..15 only) to 16, so that the per-query kernels launch 16 workgroups, not 256
+    const uint32_t qpad = nq <= kSkinnyMaxQ ? kSkinnyMaxQ : (uint32_t)round_up(nq, kFilterTile);
     BSR_TRY(qf32.ensure((size_t)qpad * ld * sizeof(float)));
     BSR_TRY(nb.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(qop.ensure((size_t)qpad * op_row_bytes));
