@@ -98,8 +98,8 @@ struct bsr_comm {
     PinnedVec<int32_t> h_hdr;      // [1 + size][kHdrWords]: this rank's words, then every rank's
     bool hdr_posted = false;       // this search's header all-gather has been issued
     // the global-threshold search (parallel_gtau): gathered sample keys, gathered result
-    // buffers, the merged result (device and pinned host), the fallback queries
-    DevBuf g_smax, g_res, m_res, fb_q, pub_ticket;
+    // buffers, the merged result (device and pinned host)
+    DevBuf g_smax, g_res, m_res, pub_ticket;
     PinnedVec<uint8_t> h_stage;
     uint8_t* h_mres = nullptr;      // fine-grained pinned: the merge kernel publishes into it
     uint8_t* h_mres_dev = nullptr;
@@ -622,6 +622,51 @@ static int allgather_device(bsr_comm* c, const void* send, void* recv, size_t by
 static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
                          uint64_t* out_idx, float* out_dist, uint32_t* out_count, bool allow_gtau);
 
+// The merged result of the global-threshold search: [fail count, NaN word | status words
+// [P][4] | fail list [nq] | counts [nq] | distances [nq][k] | indices [nq][k]]
+struct MresLayout { size_t o_st, o_fail, o_cnt, o_dist, o_idx, bytes; };
+static MresLayout mres_layout(uint32_t P, uint32_t nq, uint32_t k) {
+    const size_t nqk = (size_t)nq * k;
+    MresLayout L;
+    L.o_st = 16;
+    L.o_fail = round_up(L.o_st + (size_t)P * kStWords * 4, 16);
+    L.o_cnt = round_up(L.o_fail + (size_t)nq * 4, 16);
+    L.o_dist = round_up(L.o_cnt + (size_t)nq * 4, 16);
+    L.o_idx = round_up(L.o_dist + nqk * 4, 16);
+    L.bytes = round_up(L.o_idx + nqk * 8, 16);
+    return L;
+}
+
+// Every buffer the global-threshold search uses after the header, allocated BEFORE the header
+// is posted (after phase A, which sized the rank's result buffer): an allocation that fails here
+// takes the rank -- and so every rank -- off the path through its header, where one failing
+// between two all-gathers would leave the other ranks waiting in the next.
+static int gtau_reserve(bsr_comm* c, const bsr_index* ix, uint32_t nq, uint32_t k) {
+    const size_t P = (size_t)c->size;
+    const size_t kb = (size_t)ix->gt_qpad * ix->gt_ks * sizeof(uint64_t), rbytes = ix->res_bytes;
+    const size_t mbytes = mres_layout((uint32_t)P, nq, k).bytes;
+    BSR_HIP(hipSetDevice(ix->device));
+    BSR_TRY(c->g_smax.ensure(kb * P));
+    BSR_TRY(c->g_res.ensure(rbytes * P));
+    BSR_TRY(c->m_res.ensure(mbytes));
+    if (c->host_fn) BSR_TRY(c->h_stage.resize(std::max(kb, rbytes) * (1 + P)));
+    if (c->h_mres_bytes < mbytes) {
+        if (c->h_mres) BSR_HIP(hipHostFree(c->h_mres));
+        c->h_mres = nullptr;
+        c->h_mres_bytes = 0;
+        BSR_HIP(hipHostMalloc((void**)&c->h_mres, mbytes, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_mres_dev, c->h_mres, 0));
+        c->h_mres_bytes = mbytes;
+    }
+    if (!c->h_flag) {
+        BSR_TRY(c->pub_ticket.ensure(sizeof(uint32_t)));
+        BSR_HIP(hipMemsetAsync(c->pub_ticket.p, 0, sizeof(uint32_t), ix->stream));
+        BSR_HIP(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_flag_dev, c->h_flag, 0));
+    }
+    return BSR_OK;
+}
+
 // The rest of a parallel search with the global emission threshold, every rank
 // having enqueued phase A (query prep, sample pass, its ks best sample keys per query) and
 // every header saying so:
@@ -653,34 +698,16 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     BSR_HIP(hipSetDevice(ix->device));
     // 1. the sample keys of every rank, then phase B
     const size_t kb = (size_t)ix->gt_qpad * ix->gt_ks * sizeof(uint64_t);
-    BSR_TRY(c->g_smax.ensure(kb * P));
     BSR_TRY(allgather_device(c, ix->smax.p, c->g_smax.p, kb, s));
     BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P));
     // 2. the packed result buffers
     const size_t rbytes = ix->res_bytes;
-    BSR_TRY(c->g_res.ensure(rbytes * P));
     BSR_TRY(allgather_device(c, ix->res[ix->cur].p, c->g_res.p, rbytes, s));
-    // 3. merge + certify into m_res: [fail count, NaN word | status words [P][4] | fail list
-    //    [nq] | counts [nq] | distances [nq][k] | indices [nq][k]]
+    // 3. merge + certify into m_res (mres_layout)
     const size_t nqk = (size_t)nq * k;
-    const size_t o_st = 16, o_fail = round_up(o_st + (size_t)P * kStWords * 4, 16),
-                 o_cnt = round_up(o_fail + (size_t)nq * 4, 16), o_dist = round_up(o_cnt + (size_t)nq * 4, 16),
-                 o_idx = round_up(o_dist + nqk * 4, 16), mbytes = round_up(o_idx + nqk * 8, 16);
-    BSR_TRY(c->m_res.ensure(mbytes));
-    if (c->h_mres_bytes < mbytes) {
-        if (c->h_mres) BSR_HIP(hipHostFree(c->h_mres));
-        c->h_mres = nullptr;
-        c->h_mres_bytes = 0;
-        BSR_HIP(hipHostMalloc((void**)&c->h_mres, mbytes, hipHostMallocCoherent));
-        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_mres_dev, c->h_mres, 0));
-        c->h_mres_bytes = mbytes;
-    }
-    if (!c->h_flag) {
-        BSR_HIP(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocCoherent));
-        BSR_HIP(hipHostGetDevicePointer((void**)&c->h_flag_dev, c->h_flag, 0));
-        BSR_TRY(c->pub_ticket.ensure(sizeof(uint32_t)));
-        BSR_HIP(hipMemsetAsync(c->pub_ticket.p, 0, sizeof(uint32_t), s));
-    }
+    const MresLayout L = mres_layout(P, nq, k);
+    const size_t o_st = L.o_st, o_fail = L.o_fail, o_cnt = L.o_cnt, o_dist = L.o_dist, o_idx = L.o_idx,
+                 mbytes = L.bytes;
     __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
     uint8_t* md = c->m_res.as<uint8_t>();
     BSR_HIP(hipMemsetAsync(md, 0, 4, s));         // fail count
@@ -743,20 +770,18 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
                                  reinterpret_cast<const uint32_t*>(hm + o_fail) + nf);
         std::sort(fl.begin(), fl.end());
         const uint32_t d = ix->dim;
-        const float* fq = nullptr;
-        std::vector<float> hq;
-        if (is_device_ptr(queries)) {
-            BSR_TRY(c->fb_q.ensure((size_t)nf * d * sizeof(float)));
-            for (uint32_t i = 0; i < nf; ++i)
-                BSR_HIP(hipMemcpyAsync(c->fb_q.as<float>() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float),
-                                       hipMemcpyDeviceToDevice, s));
-            BSR_HIP(stream_wait(s));
-            fq = c->fb_q.as<float>();
-        } else {
-            hq.resize((size_t)nf * d);
-            for (uint32_t i = 0; i < nf; ++i) memcpy(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float));
-            fq = hq.data();
+        // (gathered into host memory: nothing is allocated on the device between collectives)
+        std::vector<float> hq((size_t)nf * d);
+        const bool qdev = is_device_ptr(queries);
+        for (uint32_t i = 0; i < nf; ++i) {
+            if (qdev)
+                BSR_HIP(hipMemcpyAsync(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float),
+                                       hipMemcpyDeviceToHost, s));
+            else
+                memcpy(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float));
         }
+        if (qdev) BSR_HIP(stream_wait(s));
+        const float* fq = hq.data();
         std::vector<uint64_t> fi((size_t)nf * k);
         std::vector<float> fd((size_t)nf * k);
         std::vector<uint32_t> fc(nf);
@@ -825,6 +850,7 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         if (gt) {
             const int r = ix->gtau_phase_a(queries, nq, k);  // (enqueued: the header overlaps it)
             if (r != BSR_OK) { st = r; gt = false; }
+            else if (gtau_reserve(c, ix, nq, k) != BSR_OK) gt = false;  // (the standard path then)
         }
         c->hdr_posted = false;
         const int hs = header_start(c, nq, k, st, gt, ix ? ix->n : 0, true);
