@@ -264,12 +264,12 @@ def run_c1(args):
         if st != 0:
             raise bsr.BsrError(st, lib.bsr_last_error().decode())
 
+    index.set_profile(1)  # (settle + warmup at the timed steps' profile level: the same path)
     t_end = time.perf_counter() + args.settle_ms * 1e-3
     while time.perf_counter() < t_end:
         step()
     for _ in range(args.warmup):
         step()
-    index.set_profile(1)
     index.profile(reset=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -438,8 +438,10 @@ def main():
         return v
 
     # Clock settle: the same number of untimed searches on every rank (each search is a
-    # collective for N > 1), sized on rank 0 from one search's time.
+    # collective for N > 1), sized on rank 0 from one search's time -- at the timed region's
+    # profile level, so that its searches (and their graph, warmed here) are the timed ones'.
     armed("settle + warmup steps")
+    index.set_profile(1)
     step()
     t1 = time.perf_counter()
     step()
@@ -516,9 +518,9 @@ def main():
     # configs[1] side measurement (N = 1): 1M rows, the same 1000 queries
     c1 = None
     if ix1 is not None:
+        ix1.set_profile(1)
         for _ in range(max(args.warmup, 3) + 20):
             step(ix=ix1)
-        ix1.set_profile(1)
         ix1.profile(reset=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()

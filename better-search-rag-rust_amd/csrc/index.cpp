@@ -414,7 +414,7 @@ static int filter_buffers(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k)
     ix->stats.n_candidates = kp;
     BSR_TRY(ix->tau.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(ix->cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
-    BSR_TRY(ix->cnt.ensure(((size_t)qpad + 8 * kTailCounters) * sizeof(uint32_t)));  // + the tail counters
+    BSR_TRY(ix->cnt.ensure(((size_t)qpad + 8 * kTailCounters + kGangWords) * sizeof(uint32_t)));  // + tail, gangs
     BSR_TRY(ix->cand_rows.ensure((size_t)nq * kp * sizeof(uint32_t)));
     BSR_TRY(ix->ncand.ensure((size_t)nq * sizeof(uint32_t)));
     BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));

@@ -533,7 +533,7 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 // the 1.25M-row shard, 4% slower at tau = inf, even at 10M (profiles/r04b_fab_*.txt): not kept.
 // TAILX: the dynamic tail in 8 XCD-local pools (the product, tail = 1/8); 0 = one counter per
 // query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
-template <bool EMIT, int NK, int EPI = 0, int TAILX = 8>
+template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
     constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
@@ -616,6 +616,30 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         }
     };
     auto claim = [&]() -> uint32_t { return tail_id(claim_raw()); };
+    // GANG: the n_qt workgroups of a row stream read the same tiles, on one XCD, and share them
+    // through its L2 only while they stay within a few tiles of each other.  Each static tile,
+    // wave 0 adds 1 to its 16-bit field of the stream's progress word (one 64-bit atomic, its
+    // old value = every member's count); a workgroup more than GANG tiles ahead of the slowest
+    // member sleeps a bounded while (never waits for a condition: no member can hang another).
+    // The drift grows with the stream's length: 1.97x the corpus bytes fetched at 10M rows
+    // without gangs, 1.06x with GANG = 2 (and 1.4% faster); 1.0x either way at 1.25M rows, where
+    // the atomic only costs (profiles/r04i_fab*) -- hence streams of >= kGangMinTiles tiles only.
+    const bool gang = GANG && EMIT && kStaticSched && active && p.tail != nullptr && p.n_qt >= 2 && p.n_qt <= 4 &&
+                      my_static >= kGangMinTiles;
+    unsigned long long* const gprog =
+        reinterpret_cast<unsigned long long*>(p.tail + 8 * kTailCounters) + (gang ? g0 : 0u);
+    auto gang_raw = [&]() -> unsigned long long {
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        return atomicAdd(gprog + z, 1ull << (16 * qt));
+    };
+    auto gang_throttle = [&](unsigned long long old) {
+        const uint32_t me = (uint32_t)(old >> (16 * qt)) & 0xFFFFu;
+        int lag = 0;
+        for (uint32_t j = 0; j < p.n_qt; ++j)
+            if (j != qt) lag = max(lag, (int)(int16_t)(uint16_t)(me - ((uint32_t)(old >> (16 * j)) & 0xFFFFu)));
+        for (int i = GANG; i < lag && i < GANG + 4; ++i) __builtin_amdgcn_s_sleep(32);
+    };
 
     // B fragments of the wave's two 16-query blocks, all K: fb[nb][kt] = query
     // qt*256 + 32w + 16nb + (lane & 15), bytes 64kt + 16(lane >> 4) .. +15.
@@ -849,7 +873,11 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         const bool req = dyn && t + 2 >= my_static && nxt_id != kEnd;
         uint32_t claimed = 0;
         if (req && tid == 0) claimed = claim_raw();
-        const int w0_req = (req && w == 0) ? 1 : 0;
+        // (GANG, static tiles only: the progress atomic takes the claim's place in the count)
+        const bool thr = gang && t + 2 < my_static;
+        unsigned long long gold = 0;
+        if (thr && tid == 0) gold = gang_raw();
+        const int w0_req = ((req || thr) && w == 0) ? 1 : 0;
         // SAMPLE: one scale for the tile's 128 sampled rows (a scalar load: counted in lgkmcnt,
         // it leaves the DMA stream's vmcnt waits alone)
         float sc_tile = 1.0f;
@@ -883,6 +911,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 // (the atomic completed at the kt = 3 barrier; the LDS write completes, in order,
                 // before wave 0's next fragment reads are waited for -- well before kt = 5's barrier)
                 if (kt == 4 && rb == 0 && req && tid == 0) lds_ids[t & 1] = tail_id(claimed);
+                if (GANG && kt == 4 && rb == 0 && thr && tid == 0) gang_throttle(gold);
                 // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
                 // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
                 if (bar_slice ? rb == 6 : rb == 1) {
@@ -1378,7 +1407,7 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
     if (q == 0)  // the emit filter's tail counters
-        for (uint32_t i = t; i < 8 * kTailCounters; i += blockDim.x) cnt[qpad + i] = 0;
+        for (uint32_t i = t; i < 8 * kTailCounters + kGangWords; i += blockDim.x) cnt[qpad + i] = 0;
     if (q >= qpad) return;
     if (t == 0) cnt[q] = 0;
     // (smax, the global threshold's input: the query's ks best sample keys, or none)

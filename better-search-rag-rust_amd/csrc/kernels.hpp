@@ -94,6 +94,11 @@ struct GemmArgs {
 // tile) (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + x * n_qt + qt].
 constexpr uint32_t kTailDiv = 8;
 constexpr uint32_t kTailCounters = 64;
+// Row-stream gangs of the emit filter (GANG > 0): one 64-bit progress word per row stream (its
+// n_qt <= 4 workgroups' static tile counts, 16 bits each) after the tail counters,
+// cnt[qpad + 8 * kTailCounters ...], zeroed with them.
+constexpr uint32_t kGangWords = 2 * 256;
+constexpr uint32_t kGangMinTiles = 256;  // (static tiles per row stream: ~2.5M rows and up)
 // e0 / e1 (optional): events recorded at the kernel's own dispatch and completion
 // (hipExtLaunchKernel), i.e. its device duration without the stream's launch gaps.
 hipError_t launch_filter_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,

@@ -8,6 +8,7 @@
 #   r125        the 1.25M-row shard of an 8-GPU split (the per-rank step of the scale curve)
 #   prof        rocprofv3 kernel stats of the default bench
 #   timeline    rocprofv3 kernel trace of the 1.25M shard -> per-batch kernel/gap timeline
+#   apitrace    rocprofv3 HIP API + kernel trace of the 1.25M shard (the host's share of the turnaround)
 #   pmc         HBM traffic (FETCH_SIZE, WRITE_SIZE) at 10M / 5M / 2.5M / 1.25M rows into a copy of
 #               profiles/pmc_traffic.json, then one SQ/GRBM pass at 10M
 #   pmcsmall    two SQ passes (issue, LDS, waits) over the default bench
@@ -64,6 +65,10 @@ for step in $STEPS; do
           python3 bench.py --rows 1250000 --verify 0 --steps 30 --p50-iters 3 $NOB
       f=$(find "$O/tl125" -name "*kernel_trace.csv" | head -1)
       python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_125.txt"; tail -30 "$O/timeline_125.txt" ;;
+    apitrace)
+      run 300 "hip trace 1.25M" "$O/bench_125_api.json" rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$O/api125" -o run -- \
+          python3 bench.py --rows 1250000 --verify 0 --steps 30 --p50-iters 3 $NOB
+      find "$O/api125" -name "*.csv" | head -5 ;;
     pmc)
       export PMC_RUN="$TAG"
       cp profiles/pmc_traffic.json "$O/pmc_traffic.json"

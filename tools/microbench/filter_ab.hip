@@ -36,7 +36,7 @@ int main(int argc, char** argv) {
     const int rounds = argc > 3 ? atoi(argv[3]) : 10;
     const float tau_emit = argc > 4 ? atof(argv[4]) : 0.1473f;
     const uint32_t ld = 768, qpad = (nq + 255) / 256 * 256, npad = (n + 255) / 256 * 256, cap = 1024;
-    const uint32_t n_cnt = qpad + 8 * bsr::kTailCounters;
+    const uint32_t n_cnt = qpad + 8 * bsr::kTailCounters + bsr::kGangWords;
     uint8_t *A8, *B8;
     float *tau, *as, *bs;
     uint64_t* cand;
@@ -63,10 +63,9 @@ int main(int argc, char** argv) {
 
     struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; };
     std::vector<V> vs = {
-        {"tailx0", bsr::k_filter_qs16<true, 12, 0, 0>, {}},
-        {"product", bsr::k_filter_qs16<true, 12, 0, 8>, {}},
-        {"stage", bsr::k_filter_qs16<true, 12, 2, 8>, {}},
-        {"defer", bsr::k_filter_qs16<true, 12, 1, 8>, {}},
+        {"product", bsr::k_filter_qs16<true, 12>, {}},
+        {"gang0", bsr::k_filter_qs16<true, 12, 0, 8, 0>, {}},
+        {"gang1", bsr::k_filter_qs16<true, 12, 0, 8, 1>, {}},
     };
 
     hipEvent_t e0, e1;
