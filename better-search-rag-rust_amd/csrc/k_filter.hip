@@ -621,8 +621,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     // wave 0 adds 1 to its 16-bit field of the stream's progress word (one 64-bit atomic, its
     // old value = every member's count); a workgroup more than GANG tiles ahead of the slowest
     // member sleeps a bounded while (never waits for a condition: no member can hang another).
-    // The drift grows with the stream's length: 1.97x the corpus bytes fetched at 10M rows
-    // without gangs, 1.06x with GANG = 2 (and 1.4% faster); 1.0x either way at 1.25M rows, where
+    // The drift grows with the stream's length: 2.02x the corpus bytes fetched at 10M rows
+    // without gangs, 1.09x with GANG = 2 (and 1.4% faster); 1.03x either way at 1.25M rows, where
     // the atomic only costs (profiles/r04i_fab*) -- hence streams of >= kGangMinTiles tiles only.
     const bool gang = GANG && EMIT && kStaticSched && active && p.tail != nullptr && p.n_qt >= 2 && p.n_qt <= 4 &&
                       my_static >= kGangMinTiles;
