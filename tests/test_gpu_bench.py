@@ -86,3 +86,35 @@ def _failing_run(extra=(), timeout=60):
 
 def test_bench_failing_rank_fails_fast(gpu):
     _failing_run()
+
+
+def _two_gpus():
+    try:
+        import torch  # (counting devices does not initialise the GPU)
+        return torch.cuda.device_count() >= 2
+    except Exception:
+        return False
+
+
+# The RCCL transport needs one device per rank (RCCL refuses two ranks on one device): these run
+# on a box with two or more GPUs and are skipped on the one-GPU box (the driver's 8-GPU scale run
+# exercises the same path through bench.py --gpus N).
+@pytest.mark.skipif(not _two_gpus(), reason="RCCL: one device per rank, needs >= 2 GPUs")
+def test_bench_two_ranks_rccl(gpu):
+    d = _bench("--gpus", "2", "--rows", "200000", "--verify", "2", *QUICK)
+    _common(d, 2)
+    assert "HOST" not in d["config"]["parallelism"]
+    sc = d["parity_spot_check"]
+    assert sc["indices_equal"] and sc["distance_bits_equal"]
+
+
+@pytest.mark.skipif(not _two_gpus(), reason="RCCL: one device per rank, needs >= 2 GPUs")
+def test_bench_failing_rank_fails_fast_rccl(gpu):
+    import time
+    env = dict(os.environ, BSR_BENCH_FAIL_RANK="1")
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rows", "200000", *QUICK],
+                       cwd=ROOT, capture_output=True, text=True, timeout=90, env=env)
+    assert r.returncode != 0 and time.monotonic() - t0 < 90
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["value"] is None and d["failed_rank"] == 1
