@@ -740,7 +740,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // wait for the completion signal: index.cpp flag_wait)
     ma.pub_src = md;
     ma.pub_dst = c->h_mres_dev;
-    ma.pub_bytes = mbytes;
+    ma.pub_bytes = root ? mbytes : o_cnt;  // (a non-root rank reads the status words and F only)
     ma.pub_flag = c->h_flag_dev;
     ma.pub_ticket = c->pub_ticket.as<uint32_t>();
     BSR_HIP(launch_merge(ma, s));

@@ -12,6 +12,26 @@
 #include <algorithm>
 #include <type_traits>
 
+namespace {
+// The publish copy (device result -> fine-grained host memory) by the threads t of n of one
+// workgroup: 8 loads in flight per thread before their stores (a load-store pair per trip would
+// wait out one load latency per 16 bytes x n)
+__device__ __forceinline__ void publish_copy(const uint8_t* src8, uint8_t* dst8, size_t bytes, uint32_t t, uint32_t n) {
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(src8);
+    uint4* __restrict__ dst = reinterpret_cast<uint4*>(dst8);
+    const size_t n16 = bytes / 16;
+    size_t i = t;
+    for (; i + 7 * (size_t)n < n16; i += 8 * (size_t)n) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = src[i + j * (size_t)n];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dst[i + j * (size_t)n] = v[j];
+    }
+    for (; i < n16; i += n) dst[i] = src[i];
+}
+}  // namespace
+
 namespace bsr {
 
 static inline uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap = 65536) {
@@ -408,10 +428,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         __syncthreads();
         if (s_last) {
             __threadfence();
-            const size_t n16 = a.pub_bytes / 16;
-            const uint4* src = reinterpret_cast<const uint4*>(a.pub_src);
-            uint4* dst = reinterpret_cast<uint4*>(a.pub_dst);
-            for (size_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+            publish_copy(a.pub_src, a.pub_dst, a.pub_bytes, threadIdx.x, blockDim.x);
             __threadfence_system();
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -777,10 +794,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         __syncthreads();
         if (s_last) {
             __threadfence();
-            const size_t n16 = a.pub_bytes / 16;
-            const uint4* src = reinterpret_cast<const uint4*>(a.pub_src);
-            uint4* dst = reinterpret_cast<uint4*>(a.pub_dst);
-            for (size_t i = lane; i < n16; i += kWave) dst[i] = src[i];
+            publish_copy(a.pub_src, a.pub_dst, a.pub_bytes, lane, kWave);
             __threadfence_system();
             __syncthreads();
             if (lane == 0) {
