@@ -38,10 +38,21 @@ def main():
             body.append(x)
         trimmed.append(body)
     searches = trimmed
-    steady = searches[skip:]
+    # the dominant kernel sequence only (the batched searches; single-query, profiled-stage and
+    # local-only passes have other sequences)
+    sig = collections.Counter(tuple(n.split("(")[0] for _, _, n in sr) for sr in searches[skip:])
+    main_sig = sig.most_common(1)[0][0] if sig else None
+    steady = [sr for sr in searches[skip:] if tuple(n.split("(")[0] for _, _, n in sr) == main_sig]
     if not steady:
         print("no complete searches")
         return
+    print(f"kernel sequences: {len(sig)}; the dominant one: {len(steady)} of {sum(sig.values())} searches")
+    gaps = collections.defaultdict(list)
+    for sr in steady:
+        for j in range(1, len(sr)):
+            gaps[j].append((sr[j][0] - sr[j - 1][1]) / 1e3)
+    for j in sorted(gaps):
+        print(f"  gap before {main_sig[j][:60]:60s} {statistics.median(gaps[j]):8.2f} us (median)")
     dur = collections.defaultdict(list)
     spans, busys, turns = [], [], []
     for i, sr in enumerate(steady):
