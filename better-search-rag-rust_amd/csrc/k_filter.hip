@@ -533,12 +533,18 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 // the 1.25M-row shard, 4% slower at tau = inf, even at 10M (profiles/r04b_fab_*.txt): not kept.
 // TAILX: the dynamic tail in 8 XCD-local pools (the product, tail = 1/8); 0 = one counter per
 // query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
-template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2>
+template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
-    constexpr int S = 8, A = 6;          // ring slots, slices issued ahead
+    // ring slots, slices issued ahead (RING, lab: 12 slots -- slot = slice index within the tile
+    // for NK = 12 -- with A = 9 / 10 / 6 and a smaller emission ring to fit the LDS)
+    constexpr int S = RING ? 12 : 8, A = RING == 1 ? 9 : RING == 2 ? 10 : 6;
+    // the barrier wait's DMA count (slices <= jj + 3 landed: A - 4 younger ones in flight), the
+    // last odd slice at which the tile's scale load / claim is younger than the slice waited
+    // for, and the slice after the first barrier that has them complete
+    constexpr int kWaitN = A - 4, kYoung = A - 4, kClaimUse = ((A - 4) % 2 == 0 ? A - 3 : A - 2) + 1;
     constexpr int BM = 128, BN = kFilterTile, NT = 512, SLOT = BM * kSliceB;
-    constexpr int CAP = 10;             // candidate ring entries per (lane, query block)
+    constexpr int CAP = RING ? 7 : 10;  // candidate ring entries per (lane, query block)
     static_assert(NK % 2 == 0 && NK >= 2 && NK <= 12, "even slice counts up to 768 bytes");
     // STAGE: per-query LDS lists [BN][QCAP] keys + counts, the stage of raw blocks [NSTG][1 KiB]
     // + their records [NSTG][4 words], the queries' {scale, tau} [BN][2], the stage count
@@ -910,8 +916,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
                 // (the atomic completed at the kt = 3 barrier; the LDS write completes, in order,
                 // before wave 0's next fragment reads are waited for -- well before kt = 5's barrier)
-                if (kt == 4 && rb == 0 && req && tid == 0) lds_ids[t & 1] = tail_id(claimed);
-                if (GANG && kt == 4 && rb == 0 && thr && tid == 0) gang_throttle(gold);
+                if (kt == kClaimUse && rb == 0 && req && tid == 0) lds_ids[t & 1] = tail_id(claimed);
+                if (GANG && kt == kClaimUse && rb == 0 && thr && tid == 0) gang_throttle(gold);
                 // DMA of slice jj + A: after group 1 on even slices; after the barrier (group 6)
                 // on odd slices (the slot it refills, slice jj - 2's, is then free everywhere)
                 if (bar_slice ? rb == 6 : rb == 1) {
@@ -929,7 +935,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                     // barrier alone, [6] the DMA wait)
                     if (EMIT) {
                         BSR_FST(st_a);
-                        qs_vm_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
+                        qs_vm_n(kWaitN + ((EMIT && kt <= kYoung) ? 1 + w0_req : 0));
                         BSR_FST(st_b);
                         fst[6] += st_b - st_a;
                         st_a = st_b;
@@ -938,7 +944,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                         fst[kt == 1 ? 3 : 4] += st_b - st_a;
                     } else
 #endif
-                    qs_wait_n(2 + ((EMIT && kt <= 2) ? 1 + w0_req : 0));
+                    qs_wait_n(kWaitN + ((EMIT && kt <= kYoung) ? 1 + w0_req : 0));
                 }
                 if constexpr (STAGE) {
                     // the previous tile's stage: its count read after the kt = 1 barrier (every

@@ -64,8 +64,9 @@ int main(int argc, char** argv) {
     struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; };
     std::vector<V> vs = {
         {"product", bsr::k_filter_qs16<true, 12>, {}},
-        {"gang0", bsr::k_filter_qs16<true, 12, 0, 8, 0>, {}},
-        {"gang1", bsr::k_filter_qs16<true, 12, 0, 8, 1>, {}},
+        {"ring12a6", bsr::k_filter_qs16<true, 12, 0, 8, 2, 3>, {}},
+        {"ring12a9", bsr::k_filter_qs16<true, 12, 0, 8, 2, 1>, {}},
+        {"ring12a10", bsr::k_filter_qs16<true, 12, 0, 8, 2, 2>, {}},
     };
 
     hipEvent_t e0, e1;
