@@ -209,6 +209,25 @@ def cpu_model():
     return None
 
 
+LAUNCH_TIMING = ("HIP events recorded on the index's stream around each filter launch, over K searches "
+                 "right after the timed region (kernel_timing_pass)")
+
+
+def kernel_timing_pass(index, step, n, ix_step=None):
+    """The filter kernel's launch durations for the roofline: n more searches right after the
+    timed region at profile level 1 -- HIP events recorded on the index's stream around each
+    filter launch (the search launched directly, not graph-replayed).  Event-record nodes inside a
+    replayed graph time from the graph's start, and the events hipExtLaunchKernel binds to a
+    launch start at its submission, on ROCm 7.2 (profiles/r04m_*)."""
+    index.set_profile(1)
+    index.profile(reset=True)
+    for _ in range(n):
+        step() if ix_step is None else ix_step()
+    prof = index.profile(reset=True)
+    index.set_profile(0)
+    return prof
+
+
 def run_c1(args):
     """configs[0] (the reference's own CPU/MPI plumbing case, JabRef ~20k chunks): the corpus
     lives in the reference's vector store (one parquet file, column "embeddings" of
@@ -264,22 +283,20 @@ def run_c1(args):
         if st != 0:
             raise bsr.BsrError(st, lib.bsr_last_error().decode())
 
-    index.set_profile(1)  # (settle + warmup at the timed steps' profile level: the same path)
+    index.set_profile(0)  # (settle, warmup and timed steps: the product path, graph replay)
     t_end = time.perf_counter() + args.settle_ms * 1e-3
     while time.perf_counter() < t_end:
         step()
     for _ in range(args.warmup):
         step()
-    index.profile(reset=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
-    prof = index.profile(reset=True)
     res_i, res_d, res_c = oi.copy(), od.copy(), oc.copy()
-    index.set_profile(0)
+    prof = kernel_timing_pass(index, step, args.steps)
     lat = []
     for _ in range(max(args.p50_iters, 20)):
         t1 = time.perf_counter()
@@ -441,7 +458,7 @@ def main():
     # collective for N > 1), sized on rank 0 from one search's time -- at the timed region's
     # profile level, so that its searches (and their graph, warmed here) are the timed ones'.
     armed("settle + warmup steps")
-    index.set_profile(1)
+    index.set_profile(0)  # (settle, warmup and timed steps: the product path, graph replay)
     step()
     t1 = time.perf_counter()
     step()
@@ -451,10 +468,8 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    # Timed region: exactly K searches between barriers; HIP events on the filter kernels
-    # only (bound to their dispatch: the roofline's launch durations).
-    index.set_profile(1)
-    index.profile(reset=True)
+    # Timed region: exactly K searches between barriers (the product path: graph replay, no
+    # events); the filter's launch durations come from the pass right after it.
     stats_fb = stats_rescued = 0
     barrier()
     armed("timed steps")
@@ -466,8 +481,7 @@ def main():
         stats_rescued += ls.n_rescued
     barrier()
     elapsed = time.perf_counter() - t0
-    armed("stage-profile, local-search and p50 passes")
-    prof = index.profile(reset=True)
+    armed("kernel-timing, stage-profile, local-search and p50 passes")
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -475,6 +489,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     st = index.last_stats()
     res_i, res_d, res_c = oi.copy(), od.copy(), oc.copy()  # the last timed step's result (root)
+    prof = kernel_timing_pass(index, step, args.steps)  # (every rank: each search is a collective)
     # per-stage breakdown from a separate profiled pass (every stage evented)
     index.set_profile(2)
     n_stage = max(3, min(args.steps, 10))
@@ -518,17 +533,16 @@ def main():
     # configs[1] side measurement (N = 1): 1M rows, the same 1000 queries
     c1 = None
     if ix1 is not None:
-        ix1.set_profile(1)
+        ix1.set_profile(0)
         for _ in range(max(args.warmup, 3) + 20):
             step(ix=ix1)
-        ix1.profile(reset=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
             step(ix=ix1)
         torch.cuda.synchronize()
         c1_ms = (time.perf_counter() - t1) / args.steps * 1e3
-        p1 = ix1.profile(reset=True)
+        p1 = kernel_timing_pass(ix1, None, args.steps, lambda: step(ix=ix1))
         e1 = p1.gemm_emit_ms / max(p1.gemm_emit_launches, 1)
         a1 = 2.0 * Q * 1_000_000 * D / (e1 * 1e-3) if e1 > 0 else None
         c1 = {"workload": "configs[1]: first 1M rows of the corpus, the same 1000 queries, top-10, 1 GPU",
@@ -566,7 +580,7 @@ def main():
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1) if gbs else None,
                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4) if gbs else None,
                     "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes_per_launch": sbytes,
-                    "avg_launch_ms": round(emit_ms, 5)}
+                    "avg_launch_ms": round(emit_ms, 5), "launch_timing": LAUNCH_TIMING}
         else:
             flops = 2.0 * Q * n_local * D
             achieved = flops / (emit_ms * 1e-3) / 1e12 if emit_ms > 0 else None
@@ -580,6 +594,7 @@ def main():
                     "frac": round(achieved * 1e12 / peak, 4) if achieved else None, "traffic": traffic,
                     "traffic_source": traffic_src,
                     "algorithmic_ops_per_launch": flops, "avg_launch_ms": round(emit_ms, 5),
+                    "launch_timing": LAUNCH_TIMING,
                     "note": "rank 0's shard; ops = 2 * queries * shard rows * dim (int8 multiply-adds)"}
         out = {
             "metric": "queries/sec + p50 latency, 768-d top-10 over N vectors @1/2/4/8 GPU",

@@ -145,34 +145,22 @@ static inline void ev_begin(bsr_index* ix, Events& e, int level = 2) {
 static inline void ev_end(bsr_index* ix, Events& e) {
     if (profiling(ix) && e.armed) (void)hipEventRecord(e.b, ix->stream);
 }
-// Events of one filter / scan kernel: handed to its launch (hipExtLaunchKernel records them at
-// the kernel's own dispatch and completion), so they time the kernel, not the stream gaps.
-static inline void ev_kernel(bsr_index* ix, Events& e, hipEvent_t& a, hipEvent_t& b, int level) {
-    a = b = nullptr;
-    if (profiling(ix) && ix->prof_level >= level && e.a) { a = e.a; b = e.b; e.armed = true; }
-}
-// A filter / scan kernel launch timed at profile level >= 1: inside a graph capture the events
-// are recorded on the stream around the launch (event-record nodes: the kernel plus its
-// dispatch gap), otherwise bound to the kernel's own dispatch (hipExtLaunchKernel).
+// A filter / scan kernel launch timed at profile level >= 1: HIP events recorded on the stream
+// around a direct launch (so the start event completes when the stream reaches the kernel).
+// Two other forms were measured wrong on ROCm 7.2 (profiles/r04m_*): the events bound to the
+// launch by hipExtLaunchKernel start at the kernel's submission -- behind the sample pass and
+// tau selection still running, +0.2 ms on a 5.57 ms kernel -- and event-record nodes inside a
+// replayed graph timed from the graph's start (6.12 ms).  Timed searches are therefore never
+// graph-replayed (level 0 is the product path).
 template <class F>
 static inline hipError_t launch_timed(bsr_index* ix, Events& e, F&& launch, int level = 1) {
-    if (ix->capturing) {
-        const bool timed = profiling(ix) && ix->prof_level >= level && e.a;
-        if (timed) {
-            hipError_t r = hipEventRecord(e.a, ix->stream);
-            if (r != hipSuccess) return r;
-        }
-        hipError_t r = launch((hipEvent_t) nullptr, (hipEvent_t) nullptr);
-        if (r != hipSuccess) return r;
-        if (timed) {
-            e.armed = true;
-            return hipEventRecord(e.b, ix->stream);
-        }
-        return hipSuccess;
-    }
-    hipEvent_t e0, e1;
-    ev_kernel(ix, e, e0, e1, level);
-    return launch(e0, e1);
+    const bool timed = !ix->capturing && profiling(ix) && ix->prof_level >= level && e.a;
+    if (!timed) return launch((hipEvent_t) nullptr, (hipEvent_t) nullptr);
+    hipError_t r = hipEventRecord(e.a, ix->stream);
+    if (r == hipSuccess) r = launch((hipEvent_t) nullptr, (hipEvent_t) nullptr);
+    if (r == hipSuccess) r = hipEventRecord(e.b, ix->stream);
+    e.armed = r == hipSuccess;
+    return r;
 }
 static inline void ev_collect(Events& e, double& ms, uint64_t& n, uint64_t launches) {
     if (!e.armed) return;
@@ -711,9 +699,9 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     };
     if (publish) __atomic_store_n(h_flag, 0u, __ATOMIC_RELEASE);  // (before any launch of this search)
 
-    // Every filtered batch is graph-capturable (profile level <= 1: the filter kernels' events
-    // become event-record nodes); level 2 times every stage directly.
-    const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level <= 1);
+    // Every filtered batch is graph-capturable; a timed search (profile level >= 1) launches
+    // directly, its events recorded on the stream (launch_timed).
+    const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0);
     SearchGraph& gs = graphs[cur];
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
                             warm.timed == (profiling(ix) ? prof_level : 0);
@@ -721,10 +709,6 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen &&
         gs.timed == timed_level) {
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
-        if (timed_level >= 1) {  // the captured event-record nodes ran
-            ev_emit.armed = true;
-            ev_sample.armed = gs.sampled && timed_level >= 2;
-        }
         stats.n_candidates = kp_for(k);
         ++graph_replays;
         stats.graph_replay = 1;
@@ -747,13 +731,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(BSR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level, ev_sample.armed};
+        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level};
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         ++graph_replays;
         stats.graph_replay = 1;
     } else {
         BSR_TRY(enqueue_search());
-        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, false};
+        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level};
     }
     next_status_clean = true;
     int hook_st = BSR_OK;

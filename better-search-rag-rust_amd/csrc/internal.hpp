@@ -122,8 +122,7 @@ struct bsr_index {
         uint32_t nq = 0, k = 0;
         const float* qsrc = nullptr;
         uint64_t n = 0, gen = 0;
-        int timed = 0;         // profile level it was captured at (event-record nodes at >= 1)
-        bool sampled = false;  // it contains the sample pass (its events armed on replay)
+        int timed = 0;  // profile level it was captured at (always 0: timed searches launch directly)
     };
     bool capturing = false;    // a search is being captured into a graph
     SearchGraph graphs[2];

@@ -536,6 +536,9 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
+    // EPI = 3 (lab, stagger): only waves 4-7 -- the SIMD partners of waves 0-3 -- defer their
+    // epilogue, so one wave of each SIMD runs its tile-end VALU work beside the other's MFMAs
+    constexpr bool SPLIT = EPI == 3 && EMIT;
     // ring slots, slices issued ahead (RING, lab: 12 slots -- slot = slice index within the tile
     // for NK = 12 -- with A = 9 / 10 / 6 and a smaller emission ring to fit the LDS)
     constexpr int S = RING ? 12 : 8, A = RING == 1 ? 9 : RING == 2 ? 10 : 6;
@@ -561,6 +564,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     uint32_t* const lds_ids = reinterpret_cast<uint32_t*>(lds + S * SLOT + EM_BYTES + SB_BYTES);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool dfr = DEFER || (SPLIT && wu >= 4);  // (wave-uniform) this wave defers its epilogue
     uint64_t* const lkeys = reinterpret_cast<uint64_t*>(lds + S * SLOT) + tid;
     uint32_t ecnt[2] = {0, 0};
 
@@ -894,8 +898,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
             const bool bar_slice = (kt & 1) == 1;
 #pragma unroll
             for (int rb = 0; rb < 8; ++rb) {
-                if constexpr (DEFER && EMIT && kt == 0) {
-                    if ((rb & 1) == 0 && t > 0) epi_pair(rb >> 1, sc_prev[rb >> 1], rt_prev);
+                if constexpr ((DEFER || SPLIT) && EMIT && kt == 0) {
+                    if (dfr && (rb & 1) == 0 && t > 0) epi_pair(rb >> 1, sc_prev[rb >> 1], rt_prev);
                     // pin the first MFMAs on these row blocks below the epilogue (their C = 0
                     // operand does not read the accumulators, so nothing else orders them, and
                     // hoisted above it they would need a second set of accumulators)
@@ -1074,6 +1078,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(sc_prev[i]) : "s"(sc[i]));
             asm volatile("v_mov_b32 %0, %1" : "=v"(rt_prev) : "s"(rt));
+        } else if (SPLIT && dfr) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(sc_prev[i]) : "s"(sc[i]));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(rt_prev) : "s"(rt));
         } else {
             // level 1, one ballot per tile: the lane's integer maximum over all its 32 values of
             // each query block, scored with the tile's largest (or, for a negative maximum,
@@ -1167,8 +1175,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
             }
         }
     }
-    if constexpr (DEFER && EMIT) {  // the last tile's epilogue
-        if (t > 0)
+    if constexpr ((DEFER || SPLIT) && EMIT) {  // the last tile's epilogue
+        if (dfr && t > 0)
 #pragma unroll
             for (int s = 0; s < 4; ++s) epi_pair(s, sc_prev[s], rt_prev);
     }

@@ -103,7 +103,7 @@ typedef struct {
     float row_ebound;          /* max over rows of ||a/|a| - s q||_2 (int8 quantisation) */
     uint32_t n_rescued;        /* queries certified by the second chance (all emitted rows) */
     uint32_t graph_replay;     /* 1: the search replayed a captured hipGraph (every filtered batch
-                                  from the second search of its shape on) */
+                                  from the second search of its shape on, at profile level 0) */
 } bsr_search_stats;
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts
@@ -218,8 +218,10 @@ int bsr_allgather_bytes(bsr_comm* comm, const void* send, void* recv, uint64_t b
 /* ---- diagnostics ------------------------------------------------------------------ */
 int bsr_index_last_stats(const bsr_index* ix, bsr_search_stats* out);
 int bsr_index_profile(bsr_index* ix, bsr_profile* out, int reset);
-/* Which stages of a BSR_FLAG_PROFILE index record HIP events: 0 = none (latency runs),
- * 1 = the filter / scan kernels only, 2 = every stage (the default). */
+/* Which stages of a BSR_FLAG_PROFILE index record HIP events: 0 = none (the product path:
+ * filtered batches replay a captured hipGraph), 1 = the filter / scan kernels only, 2 = every
+ * stage (the default).  At levels 1 and 2 a search launches its kernels directly, with the
+ * events recorded on the stream around them (how kernel durations are timed). */
 int bsr_index_set_profile(bsr_index* ix, int level);
 
 /* ---- synthetic data (bench / tests): U(-1,1) f32 from a counter-based hash of

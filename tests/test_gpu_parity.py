@@ -489,8 +489,9 @@ def test_large_batch_graph_replay_reads_fresh_queries(bsr_mod, oracle_mod, gpu, 
 
 
 def test_profile_levels(bsr_mod, oracle_mod, gpu):
-    """bsr_index_set_profile: level 1 times only the emit filter / scan kernels (events bound to
-    their dispatch), 2 every stage, 0 none -- results identical at every level."""
+    """bsr_index_set_profile: level 1 times only the emit filter / scan kernels (events recorded
+    on the stream around their direct launch), 2 every stage, 0 none (graph replay) -- results
+    identical at every level."""
     rng = np.random.default_rng(31)
     rows = rng.uniform(-1, 1, (30000, 768)).astype(np.float32)
     qs = rng.uniform(-1, 1, (40, 768)).astype(np.float32)

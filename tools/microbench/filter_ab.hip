@@ -5,6 +5,7 @@
 // Build: make -C tools/microbench filter_ab      Run: ./filter_ab [rows] [queries] [rounds] [tau]
 // (tau: 0.1473 emits ~256 rows per query at 10M rows, 0.1284 at 1.25M -- the product's rate)
 #include "k_filter.hip"
+#include "k_rs_lab.hip"
 
 #include <stdio.h>
 #include <string.h>
@@ -61,12 +62,24 @@ int main(int argc, char** argv) {
     const uint32_t per_xcd = g.n_qt >= 32 ? g.n_qt : (32 / g.n_qt) * g.n_qt, grid = 8 * per_xcd;
     const double ops = 2.0 * nq * (double)n * ld;
 
-    struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; };
+    // row-streaming lab kernels (k_rs_lab.hip): the corpus in the fragment-native layout, 128-query tiles
+    uint8_t* A8n;
+    CHECK(hipMalloc(&A8n, (size_t)npad * ld));
+    hipLaunchKernelGGL(bsr::lab::k_to_native, dim3(4096), dim3(256), 0, 0, A8, A8n, npad);
+    CHECK(hipDeviceSynchronize());
+    bsr::GemmArgs gr = g;
+    gr.A = A8n;
+    gr.n_qt = qpad / 128;
+    const uint32_t rs_grid = 8 * ((32 / gr.n_qt) * gr.n_qt);
+    if (32 % gr.n_qt) { printf("row-streaming lab: n_qt must divide 32\n"); return 3; }
+
+    struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; int rs = 0; };
     std::vector<V> vs = {
         {"product", bsr::k_filter_qs16<true, 12>, {}},
-        {"ring12a6", bsr::k_filter_qs16<true, 12, 0, 8, 2, 3>, {}},
-        {"ring12a9", bsr::k_filter_qs16<true, 12, 0, 8, 2, 1>, {}},
-        {"ring12a10", bsr::k_filter_qs16<true, 12, 0, 8, 2, 2>, {}},
+        {"rs12r4", bsr::lab::k_filter_rs<12, 4>, {}, 12},
+        {"rs12r6", bsr::lab::k_filter_rs<12, 6>, {}, 12},
+        {"rs16r3b3", bsr::lab::k_filter_rs<16, 3, 3>, {}, 16},
+        {"rs12r4hot", bsr::lab::k_filter_rs<12, 4, 4, 1>, {}, 12},
     };
 
     hipEvent_t e0, e1;
@@ -78,7 +91,8 @@ int main(int argc, char** argv) {
         CHECK(hipMemcpy(tau, ht.data(), qpad * 4, hipMemcpyHostToDevice));
         CHECK(hipMemset(cnt, 0, n_cnt * 4));
         CHECK(hipEventRecord(e0));
-        hipLaunchKernelGGL(v.k, dim3(grid), dim3(512), 0, 0, g);
+        if (v.rs) hipLaunchKernelGGL(v.k, dim3(rs_grid), dim3(64 * v.rs), 0, 0, gr);
+        else hipLaunchKernelGGL(v.k, dim3(grid), dim3(512), 0, 0, g);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
@@ -107,8 +121,10 @@ int main(int argc, char** argv) {
     }
     bool same = true;
     for (size_t i = 1; i < vs.size(); ++i) {
-        printf("emitted sets %s vs %s: %s\n", vs[i].name, vs[0].name, sets[0] == sets[i] ? "IDENTICAL" : "DIFFER");
-        same &= sets[0] == sets[i];
+        const bool timing_only = strstr(vs[i].name, "hot") != nullptr;  // (ablations: other data, timing only)
+        printf("emitted sets %s vs %s: %s%s\n", vs[i].name, vs[0].name, sets[0] == sets[i] ? "IDENTICAL" : "DIFFER",
+               timing_only ? " (timing-only ablation)" : "");
+        same &= timing_only || sets[0] == sets[i];
     }
     fflush(stdout);
     if (!same) return 2;
