@@ -706,8 +706,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // 3. merge + certify into m_res (mres_layout)
     const size_t nqk = (size_t)nq * k;
     const MresLayout L = mres_layout(P, nq, k);
-    const size_t o_st = L.o_st, o_fail = L.o_fail, o_cnt = L.o_cnt, o_dist = L.o_dist, o_idx = L.o_idx,
-                 mbytes = L.bytes;
+    const size_t o_st = L.o_st, o_fail = L.o_fail, o_cnt = L.o_cnt, o_dist = L.o_dist, o_idx = L.o_idx;
     __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
     uint8_t* md = c->m_res.as<uint8_t>();
     BSR_HIP(hipMemsetAsync(md, 0, 4, s));         // fail count
@@ -740,7 +739,13 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // wait for the completion signal: index.cpp flag_wait)
     ma.pub_src = md;
     ma.pub_dst = c->h_mres_dev;
-    ma.pub_bytes = root ? mbytes : o_cnt;  // (a non-root rank reads the status words and F only)
+    // (the status words and F; the root's merged rows are written through by the merging waves)
+    ma.pub_bytes = o_cnt;
+    if (root) {
+        ma.hout_idx = reinterpret_cast<uint64_t*>(c->h_mres_dev + o_idx);
+        ma.hout_dist = reinterpret_cast<float*>(c->h_mres_dev + o_dist);
+        ma.hout_count = reinterpret_cast<uint32_t*>(c->h_mres_dev + o_cnt);
+    }
     ma.pub_flag = c->h_flag_dev;
     ma.pub_ticket = c->pub_ticket.as<uint32_t>();
     BSR_HIP(launch_merge(ma, s));

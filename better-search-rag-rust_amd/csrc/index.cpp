@@ -526,6 +526,11 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     ra.res_idx = ix->d_idx;
     ra.res_dist = ix->d_dist;
     ra.res_cnt = ix->d_cnt;
+    if (publish) {  // the result rows also go straight to the host mirror (published below)
+        ra.hres_idx = reinterpret_cast<uint64_t*>(ix->h_res_dev + ix->res_off_idx);
+        ra.hres_dist = reinterpret_cast<float*>(ix->h_res_dev + ix->res_off_dist);
+        ra.hres_cnt = reinterpret_cast<uint32_t*>(ix->h_res_dev + ix->res_off_cnt);
+    }
     ra.offset = ix->global_offset;
     ra.n_rows = ix->n;
     if (fused_select) {
@@ -558,10 +563,10 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     rb.emit_cnt = ix->cnt.as<uint32_t>();
     rb.cur_status = status;
     rb.n_queries = nq;
-    if (publish) {  // the batch's last kernel: the packed result to host memory, then the flag
+    if (publish) {  // the batch's last kernel: the status words to host memory, then the flag
         rb.pub_src = ix->res[ix->cur].as<uint8_t>();
         rb.pub_dst = ix->h_res_dev;
-        rb.pub_bytes = ix->res_bytes;
+        rb.pub_bytes = kStWords * sizeof(uint32_t);  // (the rows: written through by both passes)
         rb.pub_flag = ix->h_flag_dev;
         rb.pub_ticket = ix->pub_ticket.as<uint32_t>();
     }
@@ -590,8 +595,9 @@ int bsr_index::prepare_result(uint32_t nq, uint32_t k) {
         if (h_res) BSR_HIP(hipHostFree(h_res));
         h_res = nullptr;
         h_res_bytes = 0;
-        // fine-grained: the publishing kernel writes it and the host reads it while the stream
-        // may still be finishing (its flag, not the completion signal, says the bytes are there)
+        // fine-grained: the rescore kernels write the result rows into it and the publishing
+        // kernel the status words, and the host reads it while the stream may still be
+        // finishing (the flag, not the completion signal, says the bytes are there)
         BSR_HIP(hipHostMalloc((void**)&h_res, res_bytes, hipHostMallocCoherent));
         BSR_HIP(hipHostGetDevicePointer((void**)&h_res_dev, h_res, 0));
         h_res_bytes = res_bytes;
@@ -670,11 +676,11 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     qa.qids = qids_id.as<int32_t>();
     qa.status = d_status;
     qa.with_op = use_filter;
-    // The filtered path publishes its result: its last kernel copies the packed result to the
-    // pinned host mirror and raises a host flag, which the host polls -- no D2H copy node, no
-    // wait for the stream's completion signal (a kernel boundary and a system-scope release
-    // before the copy, ~20 us per batch at the 1.25M-row shard).  Profile level 2
-    // (every stage evented) keeps the D2H copy and the stream wait.
+    // The filtered path publishes its result: the rescore kernels write every result row into
+    // the pinned host mirror as well, and the last kernel copies the status words there and
+    // raises a host flag, which the host polls -- no D2H copy node, no wait for the stream's
+    // completion signal.  Profile level 2 (every stage evented) keeps the D2H
+    // copy and the stream wait.
     const bool publish = use_filter && n > 0 && (!profiling(ix) || prof_level <= 1);
     // prep -> local search -> finalize -> one D2H copy of the packed result (graph-capturable:
     // no allocation and no host synchronisation once the buffers are sized)

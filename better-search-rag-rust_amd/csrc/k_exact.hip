@@ -408,21 +408,36 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                     if (i < a.k) {
                         const uint64_t key = L.v[e];
                         const bool has = i < cnt && key != kKeyNone;
-                        a.res_idx[(uint64_t)q * a.k + i] = has ? a.offset + key_row(key) : ~0ull;
-                        a.res_dist[(uint64_t)q * a.k + i] = has ? key_dist(key) : INFINITY;
+                        const uint64_t gi = has ? a.offset + key_row(key) : ~0ull;
+                        const float gd = has ? key_dist(key) : INFINITY;
+                        a.res_idx[(uint64_t)q * a.k + i] = gi;
+                        a.res_dist[(uint64_t)q * a.k + i] = gd;
+                        if (a.hres_idx) {
+                            a.hres_idx[(uint64_t)q * a.k + i] = gi;
+                            a.hres_dist[(uint64_t)q * a.k + i] = gd;
+                        }
                     }
                 }
-                if (lane == 0) a.res_cnt[q] = cnt;
+                if (lane == 0) {
+                    a.res_cnt[q] = cnt;
+                    if (a.hres_cnt) a.hres_cnt[q] = cnt;
+                }
             }
         }
         BSR_STAMP(W, 4);
     }
     if (a.pub_flag) {
-        // publish: every workgroup's writes released (agent scope) before its ticket; the last
-        // one acquires them, copies the packed result to host memory, releases it at system
-        // scope and raises the flag the host polls
+        // publish: every workgroup's writes released (system scope when it wrote result rows
+        // to the host mirror itself, else agent scope) before its ticket; the last one acquires
+        // them, copies pub_bytes of the packed result (with a host mirror: the status words
+        // alone) to host memory, releases it at system scope and raises the flag the host polls
+        // (a workgroup that wrote nothing -- no item, not block 0: most of the device-counted
+        // grid -- releases nothing: its fence would only write back the XCD's L2 for nothing)
         __shared__ uint32_t s_last;
-        __threadfence();
+        if (blockIdx.x == 0 || blockIdx.x < n_items) {
+            if (a.hres_idx) __threadfence_system();
+            else __threadfence();
+        }
         __syncthreads();
         if (threadIdx.x == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
         __syncthreads();
@@ -684,17 +699,25 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             }
         }
         __syncthreads();
-        uint64_t* const oi = out_idx + (uint64_t)q * k;
-        float* const od = out_dist + (uint64_t)q * k;
+        // (the merged rows also go to the host mirror when the kernel publishes through one)
+        auto put = [&](uint32_t p, uint64_t vi, float vd) {
+            out_idx[(uint64_t)q * k + p] = vi;
+            out_dist[(uint64_t)q * k + p] = vd;
+            if (a.hout_idx) {
+                a.hout_idx[(uint64_t)q * k + p] = vi;
+                a.hout_dist[(uint64_t)q * k + p] = vd;
+            }
+        };
+        auto put_count = [&](uint32_t c) {
+            out_count[q] = c;
+            if (a.hout_count) a.hout_count[q] = c;
+        };
         if (__ballot(nan)) {
             if (lane == 0) {
-                out_count[q] = 0;
+                put_count(0);
                 atomicMin(a.first_nan, q);
             }
-            for (uint32_t p = lane; p < k; p += kWave) {
-                oi[p] = ~0ull;
-                od[p] = INFINITY;
-            }
+            for (uint32_t p = lane; p < k; p += kWave) put(p, ~0ull, INFINITY);
             return;
         }
         // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
@@ -756,11 +779,10 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             got += (uint32_t)__popcll(__ballot(p < k && key != kKeyNone));
             if (p < k) {
                 const uint32_t j = (uint32_t)key;
-                oi[p] = key != kKeyNone ? s_idx[j] : ~0ull;
-                od[p] = key != kKeyNone ? s_dist[j] : INFINITY;
+                put(p, key != kKeyNone ? s_idx[j] : ~0ull, key != kKeyNone ? s_dist[j] : INFINITY);
             }
         }
-        if (lane == 0) out_count[q] = got;
+        if (lane == 0) put_count(got);
         const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
         if (a.excl && lane == 0) {
             // Certification of a global-threshold parallel search: every row left
@@ -785,10 +807,11 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     };
     merge_query();
     if (a.pub_flag) {
-        // publish (as k_rescore's): the last workgroup copies the merged result to host memory
-        // and raises the host's flag
+        // publish (as k_rescore's): the last workgroup copies the merged result (with a host
+        // mirror of the rows: the part before them) to host memory and raises the host's flag
         __shared__ uint32_t s_last;
-        __threadfence();
+        if (a.hout_idx) __threadfence_system();
+        else __threadfence();
         __syncthreads();
         if (lane == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
         __syncthreads();

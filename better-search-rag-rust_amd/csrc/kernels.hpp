@@ -168,6 +168,12 @@ struct RescoreArgs {
     float* res_dist;
     uint32_t* res_cnt;          // [nq]
     uint64_t offset, n_rows;    // global index of local row 0; shard rows (count = min(k, n))
+    // (optional) the host mirror of the same rows (fine-grained pinned memory): every result row
+    // is written there too, by the wave that finalizes it, so the publish copies only the status
+    // words (the standard path; the global-threshold path publishes its whole buffer)
+    uint64_t* hres_idx;
+    float* hres_dist;
+    uint32_t* hres_cnt;
     // mode B: block 0 also zeroes the NEXT search's status words and sums the emitted counts
     // into cur_status[kStEmitted] (what k_finalize does on the other paths)
     uint32_t* next_status;
@@ -234,6 +240,11 @@ struct MergeArgs {
     const uint32_t* st;
     uint64_t st_stride;
     uint32_t* st_all;
+    // (optional) the host mirror of out_idx / out_dist / out_count: the merged rows are written
+    // there too, by the wave that merges them (pub_bytes then covers the part before them)
+    uint64_t* hout_idx;
+    float* hout_dist;
+    uint32_t* hout_count;
     // (optional) publish the merged result buffer to host memory, as RescoreArgs::pub_*
     const uint8_t* pub_src;
     uint8_t* pub_dst;
