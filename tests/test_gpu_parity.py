@@ -326,6 +326,36 @@ def test_overflowing_rows_force_exact(bsr_mod, oracle_mod, gpu):
     _assert_same(got, oracle_mod.parallel_top_k(rows, qs, 10), "overflow")
 
 
+def test_published_rescue_and_fallback_rows(bsr_mod, oracle_mod, gpu):
+    """The published result (rescore kernels writing every row into the pinned host mirror, the
+    last kernel copying only the status words, round 4) with all three sources of rows in one
+    batch, replayed as a graph: rows certified by the first rescore, rows of queries rescued by
+    the second chance (200 near-duplicates of the query: the first pass's k' candidates cannot
+    be certified), and rows of queries whose emitted list overflows (1500 near-duplicates: the
+    exact scan, read back by a D2H copy over the same host buffer)."""
+    rng = np.random.default_rng(404)
+    n, dim, nq, k = 60000, 768, 64, 10
+    rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
+    qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
+    perm = rng.permutation(n)
+    at = 0
+    for q, m in [(q, 200) for q in range(16)] + [(q, 1500) for q in range(16, 20)]:
+        pos = perm[at:at + m]
+        at += m
+        rows[pos] = qs[q] + rng.normal(0, 1e-3, (m, dim)).astype(np.float32)
+    ix = _index(bsr_mod, rows, max_k=64)
+    want = oracle_mod.parallel_top_k(rows, qs, k, size=4, threads=4)
+    rescued = fallback = replays = 0
+    for rep in range(3):
+        got = ix.local_top_k(qs, k)
+        st = ix.last_stats()
+        rescued += st.n_rescued
+        fallback += st.n_fallback
+        replays += st.graph_replay
+        _assert_same(got, want, f"rep {rep}")
+    assert rescued > 0 and fallback > 0 and replays > 0, (rescued, fallback, replays)
+
+
 def test_bf16_filter_operand_retired(bsr_mod, gpu):
     # the bf16 filter OPERAND (rounds 1-3) is retired; a bf16 CORPUS is served on the int8 filter
     with pytest.raises(bsr_mod.BsrError) as e:
