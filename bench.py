@@ -213,16 +213,17 @@ LAUNCH_TIMING = ("HIP events recorded on the index's stream around each filter l
                  "right after the timed region (kernel_timing_pass)")
 
 
-def kernel_timing_pass(index, step, n, ix_step=None):
-    """The filter kernel's launch durations for the roofline: n more searches right after the
-    timed region at profile level 1 -- HIP events recorded on the index's stream around each
-    filter launch (the search launched directly, not graph-replayed).  Event-record nodes inside a
-    replayed graph time from the graph's start, and the events hipExtLaunchKernel binds to a
-    launch start at its submission, on ROCm 7.2 (profiles/r04m_*)."""
+def kernel_timing_pass(index, search, n):
+    """The filter kernel's launch durations for the roofline: n more searches (search() runs
+    one) right after the timed region, at profile level 1 -- HIP events recorded on the index's
+    stream around each filter launch (the search launched directly, not graph-replayed).
+    Event-record nodes inside a replayed graph time from the graph's start, and the events
+    hipExtLaunchKernel binds to a launch start at its submission, on ROCm 7.2
+    (profiles/r04m_event_timing.txt)."""
     index.set_profile(1)
     index.profile(reset=True)
     for _ in range(n):
-        step() if ix_step is None else ix_step()
+        search()
     prof = index.profile(reset=True)
     index.set_profile(0)
     return prof
@@ -542,7 +543,7 @@ def main():
             step(ix=ix1)
         torch.cuda.synchronize()
         c1_ms = (time.perf_counter() - t1) / args.steps * 1e3
-        p1 = kernel_timing_pass(ix1, None, args.steps, lambda: step(ix=ix1))
+        p1 = kernel_timing_pass(ix1, lambda: step(ix=ix1), args.steps)
         e1 = p1.gemm_emit_ms / max(p1.gemm_emit_launches, 1)
         a1 = 2.0 * Q * 1_000_000 * D / (e1 * 1e-3) if e1 > 0 else None
         c1 = {"workload": "configs[1]: first 1M rows of the corpus, the same 1000 queries, top-10, 1 GPU",
