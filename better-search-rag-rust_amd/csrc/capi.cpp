@@ -659,8 +659,8 @@ static int gtau_reserve(bsr_comm* c, const bsr_index* ix, uint32_t nq, uint32_t 
         c->h_mres_bytes = mbytes;
     }
     if (!c->h_flag) {
-        BSR_TRY(c->pub_ticket.ensure(sizeof(uint32_t)));
-        BSR_HIP(hipMemsetAsync(c->pub_ticket.p, 0, sizeof(uint32_t), ix->stream));
+        BSR_TRY(c->pub_ticket.ensure(kTicketWords * sizeof(uint32_t)));
+        BSR_HIP(hipMemsetAsync(c->pub_ticket.p, 0, kTicketWords * sizeof(uint32_t), ix->stream));
         BSR_HIP(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocCoherent));
         BSR_HIP(hipHostGetDevicePointer((void**)&c->h_flag_dev, c->h_flag, 0));
     }

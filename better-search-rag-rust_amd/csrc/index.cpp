@@ -607,8 +607,8 @@ int bsr_index::prepare_result(uint32_t nq, uint32_t k) {
         BSR_HIP(hipHostMalloc((void**)&h_flag, 64, hipHostMallocCoherent));
         BSR_HIP(hipHostGetDevicePointer((void**)&h_flag_dev, h_flag, 0));
         *h_flag = 0;
-        BSR_TRY(pub_ticket.ensure(sizeof(uint32_t)));
-        BSR_HIP(hipMemsetAsync(pub_ticket.p, 0, sizeof(uint32_t), stream));
+        BSR_TRY(pub_ticket.ensure(kTicketWords * sizeof(uint32_t)));
+        BSR_HIP(hipMemsetAsync(pub_ticket.p, 0, kTicketWords * sizeof(uint32_t), stream));
         ++g_alloc_gen;
     }
     cur ^= 1u;

@@ -30,6 +30,32 @@ __device__ __forceinline__ void publish_copy(const uint8_t* src8, uint8_t* dst8,
     }
     for (; i < n16; i += n) dst[i] = src[i];
 }
+// A result value into the pinned host mirror: a system-scope store (written through, never left
+// in an L2), so that the writing wave's s_waitcnt vmcnt(0) is all the host needs before the flag
+__device__ __forceinline__ void host_put(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void host_put(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void host_put(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The publishing kernels' "who arrived last" (one thread per workgroup, after the workgroup's
+// release): an add to the workgroup's leaf counter (blockIdx % 8), and for the last of a leaf an
+// add to the root -- the workgroups of a launch split over 9 lines instead of queueing on one
+// (1000 adds to one word are the larger part of a 1000-workgroup publish).  The last workgroup
+// to arrive zeroes the counters for the next launch (the stream orders it before that launch).
+__device__ bool last_arrival(uint32_t* ticket) {
+    constexpr uint32_t L = bsr::kTicketLeaves, S = bsr::kTicketStride;
+    const uint32_t nb = gridDim.x, leaf = blockIdx.x % L;
+    const uint32_t in_leaf = (nb - leaf + L - 1) / L;  // workgroups b < nb with b % L == leaf
+    if (atomicAdd(ticket + leaf * S, 1u) != in_leaf - 1) return false;
+    const uint32_t leaves = nb < L ? nb : L;
+    if (atomicAdd(ticket + L * S, 1u) != leaves - 1) return false;
+    for (uint32_t i = 0; i <= L; ++i) ticket[i * S] = 0u;
+    return true;
+}
 }  // namespace
 
 namespace bsr {
@@ -126,6 +152,10 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     float* const lds = lds_all + w * STAGE;
     float* const ldq_all = lds_all + W * STAGE;
     const uint32_t n_items = a.n_items_dev ? *a.n_items_dev : a.n_items;
+    // (publish) this workgroup wrote state the publishing workgroup reads: the status words
+    // (block 0) or a failure list entry
+    __shared__ uint32_t s_wrote;
+    if (threadIdx.x == 0) s_wrote = blockIdx.x == 0 ? 1u : 0u;
     if ((W > 1 || a.excl_out) && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
         // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
         if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
@@ -395,6 +425,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                 if (!ok) {
                     const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
                     a.fail_list[pos] = q;
+                    s_wrote = 1u;
                 }
                 certified = ok;
             }
@@ -413,14 +444,14 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                         a.res_idx[(uint64_t)q * a.k + i] = gi;
                         a.res_dist[(uint64_t)q * a.k + i] = gd;
                         if (a.hres_idx) {
-                            a.hres_idx[(uint64_t)q * a.k + i] = gi;
-                            a.hres_dist[(uint64_t)q * a.k + i] = gd;
+                            host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
+                            host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
                         }
                     }
                 }
                 if (lane == 0) {
                     a.res_cnt[q] = cnt;
-                    if (a.hres_cnt) a.hres_cnt[q] = cnt;
+                    if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
                 }
             }
         }
@@ -431,15 +462,16 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         // to the host mirror itself, else agent scope) before its ticket; the last one acquires
         // them, copies pub_bytes of the packed result (with a host mirror: the status words
         // alone) to host memory, releases it at system scope and raises the flag the host polls
-        // (a workgroup that wrote nothing -- no item, not block 0: most of the device-counted
-        // grid -- releases nothing: its fence would only write back the XCD's L2 for nothing)
+        // Only a workgroup that wrote what the last one reads releases it (an agent fence writes
+        // back its XCD's L2): block 0's status words, a failure entry -- and, without a host
+        // mirror, the result rows it wrote.  The others only wait for their own host stores
+        // (system scope: complete at vmcnt(0)) before their ticket.
         __shared__ uint32_t s_last;
-        if (blockIdx.x == 0 || blockIdx.x < n_items) {
-            if (a.hres_idx) __threadfence_system();
-            else __threadfence();
-        }
+        __syncthreads();  // (s_wrote final)
+        if (s_wrote || (!a.hres_idx && blockIdx.x < n_items)) __threadfence();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        if (threadIdx.x == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
         __syncthreads();
         if (s_last) {
             __threadfence();
@@ -447,7 +479,6 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             __threadfence_system();
             __syncthreads();
             if (threadIdx.x == 0) {
-                *a.pub_ticket = 0u;
                 __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
@@ -669,11 +700,11 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
-    auto merge_query = [&]() {
+    auto merge_query = [&]() -> bool {
         if (a.st_all && q == 0)  // every list's status words, compact
             for (uint32_t i = lane; i < P * kStWords; i += kWave)
                 a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
-        if (q >= nq) return;
+        if (q >= nq) return false;
         // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
         const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
         uint32_t incl = c_l;
@@ -704,13 +735,13 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             out_idx[(uint64_t)q * k + p] = vi;
             out_dist[(uint64_t)q * k + p] = vd;
             if (a.hout_idx) {
-                a.hout_idx[(uint64_t)q * k + p] = vi;
-                a.hout_dist[(uint64_t)q * k + p] = vd;
+                host_put(a.hout_idx + (uint64_t)q * k + p, vi);
+                host_put(a.hout_dist + (uint64_t)q * k + p, vd);
             }
         };
         auto put_count = [&](uint32_t c) {
             out_count[q] = c;
-            if (a.hout_count) a.hout_count[q] = c;
+            if (a.hout_count) host_put(a.hout_count + q, c);
         };
         if (__ballot(nan)) {
             if (lane == 0) {
@@ -718,7 +749,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
                 atomicMin(a.first_nan, q);
             }
             for (uint32_t p = lane; p < k; p += kWave) put(p, ~0ull, INFINITY);
-            return;
+            return true;
         }
         // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
         // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
@@ -784,6 +815,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         }
         if (lane == 0) put_count(got);
         const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
+        bool shared = false;
         if (a.excl && lane == 0) {
             // Certification of a global-threshold parallel search: every row left
             // out on rank l lies at a distance >= excl_l[q] (its kernel's bound, rounded down), so
@@ -802,18 +834,25 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
                 ok = xmin == INFINITY;
             }
             if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
+            shared = !ok;
         }
-
+        return __shfl((int)shared, 0, kWave) != 0 || (a.st_all && q == 0);
     };
-    merge_query();
+    // (publish) whether this wave wrote state the publishing workgroup reads: the status words
+    // (q = 0), a failure entry, the lowest NaN query
+    const bool wrote = merge_query();
     if (a.pub_flag) {
         // publish (as k_rescore's): the last workgroup copies the merged result (with a host
         // mirror of the rows: the part before them) to host memory and raises the host's flag
+        // Only a wave that wrote what the last one copies releases it (an agent fence writes back
+        // its XCD's L2); the rows count when no host mirror takes them and the copy covers them.
+        // The others only wait for their own host stores (system scope) before their ticket.
         __shared__ uint32_t s_last;
-        if (a.hout_idx) __threadfence_system();
-        else __threadfence();
+        const bool rows_copied = !a.hout_idx && a.pub_src + a.pub_bytes > reinterpret_cast<const uint8_t*>(out_count);
+        if (wrote || rows_copied) __threadfence();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (lane == 0) s_last = atomicAdd(a.pub_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+        if (lane == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
         __syncthreads();
         if (s_last) {
             __threadfence();
@@ -821,7 +860,6 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             __threadfence_system();
             __syncthreads();
             if (lane == 0) {
-                *a.pub_ticket = 0u;
                 __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }

@@ -194,8 +194,12 @@ struct RescoreArgs {
     uint8_t* pub_dst;
     size_t pub_bytes;
     uint32_t* pub_flag;
-    uint32_t* pub_ticket;       // device word, 0 between launches
+    uint32_t* pub_ticket;       // kTicketWords device words, 0 between launches
 };
+// The publishing kernels' arrival ticket: kTicketLeaves leaf counters and one root counter,
+// each on a 64-byte line of its own (a workgroup adds to its leaf, blockIdx % kTicketLeaves; the
+// last of a leaf adds to the root), all zero between launches.
+constexpr uint32_t kTicketLeaves = 8, kTicketStride = 16, kTicketWords = (kTicketLeaves + 1) * kTicketStride;
 // Workgroups of the device-counted rescore (failed certifications, usually a few queries).
 constexpr uint32_t kRescoreAllGrid = 128;
 // Candidate lists up to this many keys (k <= 10) are selected inside the rescore kernel.
