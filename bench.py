@@ -632,6 +632,12 @@ def main():
             "roofline": roof,
             "local_search_ms_per_step": round(local_ms, 4),
             "exchange_ms_per_step": round(ms_per_step - local_ms, 4) if world > 1 else None,
+            "step_split_note": None if world == 1 else (
+                "local_search_ms_per_step = the same K searches through bsr_local_top_k (each rank's standard "
+                "local search with its own threshold, no exchange)" + (
+                    "; the timed steps ran the global-threshold search, whose local work is smaller (fewer rows "
+                    "emitted per rank), so exchange_ms_per_step understates the all-gathers + merge"
+                    if not st.n_candidates else "")),
             "kernels_ms_per_step_rank0": {  # separate profiled pass of n_stage steps (every stage evented)
                 "filter_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
                 "filter_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
