@@ -684,9 +684,8 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     const bool publish = use_filter && n > 0 && (!profiling(ix) || prof_level <= 1);
     // prep -> local search -> finalize -> one D2H copy of the packed result (graph-capturable:
     // no allocation and no host synchronisation once the buffers are sized)
-    // (with_prep = false: the query prep is launched directly, ahead of the graph -- below)
-    auto enqueue_search = [&](bool with_prep) -> int {
-        if (with_prep) BSR_HIP(launch_query_prep(qa, stream));
+    auto enqueue_search = [&]() -> int {
+        BSR_HIP(launch_query_prep(qa, stream));
         if (n == 0) {
             // Empty shard (e.g. a rank whose interval_by_rank block is empty): no results.
             BSR_HIP(hipMemsetAsync(keys.p, 0xff, (size_t)nq * k * sizeof(uint64_t), stream));
@@ -713,12 +712,8 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
                             warm.timed == (profiling(ix) ? prof_level : 0);
     const int timed_level = profiling(ix) ? prof_level : 0;
-    // A replayed graph's first kernel starts ~13 us after hipGraphLaunch is called (its launch
-    // takes ~30 us of host time); the query prep, launched directly first, runs in that window
-    // (profiles/r04y_*: the host turnaround's split).
     if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen &&
         gs.timed == timed_level) {
-        BSR_HIP(launch_query_prep(qa, stream));
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         stats.n_candidates = kp_for(k);
         ++graph_replays;
@@ -726,11 +721,10 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     } else if (graphable && same_shape && warm.gen == g_alloc_gen) {
         // capture (every buffer already sized by the direct search of this shape), then replay
         if (gs.exec) { (void)hipGraphExecDestroy(gs.exec); gs.exec = nullptr; }
-        BSR_HIP(launch_query_prep(qa, stream));
         BSR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         const uint64_t gen0 = g_alloc_gen;
         capturing = true;
-        const int rc = enqueue_search(false);
+        const int rc = enqueue_search();
         capturing = false;
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(stream, &graph);
@@ -748,7 +742,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
         ++graph_replays;
         stats.graph_replay = 1;
     } else {
-        BSR_TRY(enqueue_search(true));
+        BSR_TRY(enqueue_search());
         if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level};
     }
     next_status_clean = true;
