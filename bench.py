@@ -15,6 +15,11 @@ Usage: python bench.py [--gpus N --steps K --warmup W]
   the environment, bench.py starts the N rank processes itself (before any GPU call).
   --comm host: the exchange over gloo instead of RCCL (ranks may then share a GPU: a
   multi-rank rehearsal on a one-GPU box).
+  --comm loopback --gpus N: ONE process timing rank 0's step of an N-rank run on one GPU, every
+  all-gather emulated by a device kernel where ncclAllGather sits (bsr_comm_init_loopback), its
+  contributions replayed from a recording of a real N-rank run of the same batch (made first,
+  over the host transport with N rank processes on the one GPU; --replay FILE reuses one).  Not a
+  scaling measurement: the collectives' own latency is not in it.
 """
 import argparse
 import json
@@ -65,7 +70,11 @@ def parse():
     ap.add_argument("--queries", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--dim", type=int, default=768)
-    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl")
+    ap.add_argument("--comm", choices=["rccl", "host", "loopback"], default="rccl")
+    ap.add_argument("--replay", default=None, help="--comm loopback: a recording made by --record-gathers")
+    ap.add_argument("--record-gathers", default=None,
+                    help="--comm host, rank 0: record the first search's all-gathers to this .npz")
+    ap.add_argument("--record-only", action="store_true", help="with --record-gathers: stop after recording")
     ap.add_argument("--p50-iters", type=int, default=20)
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed searches before the warmup steps (setup): the GPU leaves its idle "
@@ -337,13 +346,37 @@ def run_c1(args):
     return 0 if (ok_i and ok_d) else 1
 
 
+def record_for_loopback(args):
+    """--comm loopback without --replay: record a real N-rank run's all-gathers first (N rank
+    processes over the host transport on this GPU; nothing here touches the GPU)."""
+    path = os.path.join(tempfile.mkdtemp(prefix="bsr_loopback_"), "gathers.npz")
+    cmd = [sys.executable, os.path.abspath(__file__), "--comm", "host", "--gpus", str(args.gpus), "--config",
+           args.config, "--record-gathers", path, "--record-only", "--dim", str(args.dim), "--queries",
+           str(args.queries), "--k", str(args.k), "--settle-ms", "0", "--warmup", "0", "--steps", "1"]
+    if args.rows is not None:
+        cmd += ["--rows", str(args.rows)]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE)
+    if r.returncode != 0 or not os.path.exists(path):
+        _error_line(args, f"recording the {args.gpus}-rank all-gathers failed (rc {r.returncode})")
+        sys.exit(r.returncode or 1)
+    return path
+
+
 def main():
     args = parse()
     if args.config == "c1":
         sys.exit(run_c1(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    loop = args.comm == "loopback"
+    if loop and world > 1:
+        _error_line(args, "--comm loopback is one process (rank 0 of --gpus N); do not launch it with torchrun")
+        sys.exit(2)
+    if loop and args.gpus > 1 and not args.replay:
+        args.replay = record_for_loopback(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not loop:
         sys.exit(spawn_ranks(args))
+    P = args.gpus if loop else world  # ranks the corpus is sharded over (loopback: emulated)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -393,8 +426,8 @@ def main():
             watchdog.arm(label, args.collective_timeout)
 
     D, Q, K = args.dim, args.queries, args.k
-    n_total = args.rows_total * (world if args.scaling == "weak" else 1)
-    iv = bsr.interval_by_rank(rank, world, n_total)
+    n_total = args.rows_total * (P if args.scaling == "weak" else 1)
+    iv = bsr.interval_by_rank(rank, P, n_total)
     start, n_local = iv.start_index, iv.get_count()
 
     # Corpus shard, generated on this GPU (never crosses PCIe), loaded into the index
@@ -428,7 +461,13 @@ def main():
 
     comm = None
     armed("communicator setup")
-    if world > 1:
+    lb_calls = 0
+    if loop and P > 1:
+        rec = np.load(args.replay)
+        script = [rec[f"rec{i}"] for i in range(int(rec["n_rec"]))]
+        lb_calls = len(script)
+        comm = bsr.Comm.loopback(0, P, device, script)
+    elif world > 1:
         if args.comm == "host":
             comm = bsr.Comm.host(dist.group.WORLD)
         else:
@@ -460,6 +499,21 @@ def main():
     # profile level, so that its searches (and their graph, warmed here) are the timed ones'.
     armed("settle + warmup steps")
     index.set_profile(0)  # (settle, warmup and timed steps: the product path, graph replay)
+    if args.record_gathers and comm is not None and comm.transport == "host":
+        comm.record = [] if rank == 0 else None
+        step()
+        n_rec = len(comm.record) if rank == 0 else 0
+        if rank == 0:
+            np.savez(args.record_gathers, n_rec=np.int32(n_rec), **{f"rec{i}": b for i, b in enumerate(comm.record)})
+        comm.record = None
+        if args.record_only:
+            barrier()
+            if rank == 0:
+                print(json.dumps({"recorded": args.record_gathers, "calls": n_rec, "ranks": world}), flush=True)
+            comm.close()
+            index.close()
+            dist.destroy_process_group()
+            return
     step()
     t1 = time.perf_counter()
     step()
@@ -602,6 +656,15 @@ def main():
             "value": round(Q / (ms_per_step * 1e-3), 2),
             "unit": "queries/s",
             "n_gpus": world,
+            "loopback": None if not loop else {
+                "ranks": P, "replayed_allgathers": comm.loopback_stats()[0] if comm else 0,
+                "missed_allgathers": comm.loopback_stats()[1] if comm else 0, "recorded_calls_per_search": lb_calls,
+                "note": (f"ONE process on one GPU timing rank 0's step of a {P}-rank run: its shard "
+                         f"({n_local} rows), every all-gather one device kernel where ncclAllGather sits "
+                         "(no host wait), the other ranks' contributions replayed from a real "
+                         f"{P}-rank run of this batch (host transport). value = queries / this step: a "
+                         "per-rank step projection without the collectives' latency, not a scaling "
+                         "measurement")},
             "steps": args.steps,
             "warmup": args.warmup,
             "settle_ms": args.settle_ms,
@@ -616,9 +679,10 @@ def main():
             "config": {
                 "workload": args.label + ("" if args.rows is None else f" (rows overridden: {n_total})"),
                 "rows_total": n_total, "rows_per_gpu_rank0": n_local, "queries": Q, "top_k": K, "dim": D,
-                "parallelism": f"corpus sharded over {world} GPU(s) (interval_by_rank)" +
-                               ("" if world == 1 else f" + {args.comm.upper()} all-gather of the partial lists"
-                                                      " + root merge"),
+                "parallelism": (f"corpus sharded over {world} GPU(s) (interval_by_rank)" +
+                                ("" if world == 1 else f" + {args.comm.upper()} all-gather of the partial lists"
+                                                       " + root merge")) if not loop else
+                               f"rank 0 of {P} (interval_by_rank), loopback communicator: emulated all-gathers",
                 "filter": "int8 MFMA (v_mfma_i32_16x16x64_i8) candidates, " + (
                     f"exact sequential-f32 rescore of k'={st.n_candidates} per query, certified (DESIGN.md §4)"
                     if st.n_candidates else
@@ -676,6 +740,8 @@ def main():
     # the corpus is regenerated 1M rows at a time on rank 0's GPU (the same counter-based
     # generator), each block's oracle lists merged as the reference merges rank blocks.
     # Then the CPU baseline (rank 0, N = 1).  Other ranks wait at the final barrier.
+    if loop:
+        args.no_cpu_baseline = True
     if rank == 0 and (args.verify or (world == 1 and not args.no_cpu_baseline)):
         import oracle
         q_h = qdev.cpu().numpy()

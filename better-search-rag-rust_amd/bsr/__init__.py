@@ -37,7 +37,7 @@ import numpy as np
 _PKG = os.path.dirname(os.path.abspath(__file__))
 # (BSR_LIB: another build of the same ABI, for A/B measurements)
 LIB_PATH = os.environ.get("BSR_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libbsr.so")
-VSTORE_LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libbsr_vstore.so")
+VSTORE_LIB_PATH = os.environ.get("BSR_VSTORE_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libbsr_vstore.so")
 
 BSR_OK = 0
 BSR_PARTIAL = 1  # parallel search root: valid result without its own block (include/bsr.h)
@@ -126,6 +126,8 @@ def lib() -> ctypes.CDLL:
         "bsr_gather_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
         "bsr_comm_init_host": (ctypes.c_int, [i32, i32, _HOST_ALLGATHER, _P, ctypes.POINTER(_P)]),
         "bsr_gather_global_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
+        "bsr_comm_init_loopback": (ctypes.c_int, [i32, i32, i32, u32, _P, _P, ctypes.POINTER(_P)]),
+        "bsr_comm_loopback_stats": (ctypes.c_int, [_P, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "bsr_broadcast": (ctypes.c_int, [_P, _P, u64, i32]),
         "bsr_allgather_bytes": (ctypes.c_int, [_P, _P, _P, u64]),
         "bsr_parallel_top_k_similarity_search": (ctypes.c_int, [_P, _P, _P, u32, u32, _P, _P, _P]),
@@ -349,6 +351,8 @@ class Comm:
 
     @classmethod
     def host(cls, group=None) -> "Comm":
+        """`record` (attribute): set it to a list and every all-gather appends its receive
+        buffer [size * bytes] to it (the script of Comm.loopback)."""
         import torch
         import torch.distributed as dist
 
@@ -365,11 +369,14 @@ class Comm:
                 for r, p in enumerate(parts):
                     if n:
                         dst[r * n:(r + 1) * n] = p.numpy()
+                if self.record is not None and n:
+                    self.record.append(dst.copy())
                 return 0
             except Exception:  # the library reports a transport failure
                 return 1
 
         self = cls.__new__(cls)
+        self.record = None
         self._cb = _HOST_ALLGATHER(allgather)  # kept alive as long as the comm
         h = _P()
         _check(lib().bsr_comm_init_host(rank, size, self._cb, None, ctypes.byref(h)))
@@ -378,6 +385,32 @@ class Comm:
         self.size = size
         self.transport = "host"
         return self
+
+    @classmethod
+    def loopback(cls, rank: int, size: int, device: int = -1, script=None) -> "Comm":
+        """One process acting as rank `rank` of `size` (measurement and tests): every
+        all-gather is one device kernel on the stream where ncclAllGather would sit.  `script`
+        (optional): the all-gathers of one parallel search recorded in a real size-rank run,
+        a list of [size * bytes] uint8 arrays in call order (see Comm.host's `record`); the
+        searches then replay them, this rank's own slot live (include/bsr.h)."""
+        script = list(script or [])
+        nb = np.array([len(x) // size for x in script] or [0], np.uint64)
+        data = np.ascontiguousarray(np.concatenate([np.frombuffer(bytes(x), np.uint8) for x in script])
+                                    if script else np.zeros(1, np.uint8))
+        self = cls.__new__(cls)
+        h = _P()
+        _check(lib().bsr_comm_init_loopback(rank, size, device, len(script), _ptr(nb), _ptr(data), ctypes.byref(h)))
+        self._h = h
+        self.rank = rank
+        self.size = size
+        self.transport = "loopback"
+        return self
+
+    def loopback_stats(self) -> Tuple[int, int]:
+        """(all-gathers replayed from the script, calls that missed it) of a loopback Comm."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().bsr_comm_loopback_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     @staticmethod
     def unique_id() -> bytes:
@@ -578,28 +611,50 @@ def parallel_top_k_similarity_search_batch(world, index: Optional[Index], querie
     """The same for a batch of queries [Q, dim] (host array or device tensor): Q independent
     reference searches in one collective call.  Root: (idx [Q, top_k] u64, dist [Q, top_k]
     f32, count [Q] u32); other ranks: None.  A non-root rank whose local step fails raises
-    after the exchange; the root then warns and returns the other ranks' global top-k."""
+    after the exchange; the root then warns and returns the other ranks' global top-k.
+    Local argument checks never return before the collective: a rank whose
+    queries are unusable still takes part, with an empty contribution (the library's null-index
+    path), and raises -- or, on the root, warns -- afterwards, as the library does for a failed
+    local search (src/mpi_helpers/metrics.rs:185-202)."""
     comm = _as_comm(world)
     if rank is None:
         rank = comm.rank if comm is not None else ROOT
+    err = None  # (status, message) of this rank's local checks
     if isinstance(queries, np.ndarray) or not hasattr(queries, "data_ptr"):
-        queries = np.ascontiguousarray(queries, np.float32)
+        try:
+            queries = np.ascontiguousarray(queries, np.float32)
+        except (TypeError, ValueError) as e:
+            err, queries = (-1, f"queries are not a float32 array: {e}"), np.zeros((0, 0), np.float32)
     if queries.ndim == 1:
         queries = queries.reshape(1, -1)
-    if queries.ndim != 2:
-        raise BsrError(-1, f"queries must be [Q, dim]; got shape {tuple(queries.shape)}")
-    if not isinstance(queries, np.ndarray):
+    if err is None and queries.ndim != 2:
+        err = (-1, f"queries must be [Q, dim]; got shape {tuple(queries.shape)}")
+    if err is None and not isinstance(queries, np.ndarray):
         import torch
         if queries.dtype != torch.float32 or not queries.is_contiguous():
-            raise BsrError(-1, "query tensors must be contiguous float32")
-    if index is not None and int(queries.shape[1]) != index.dim:
-        raise BsrError(-6, f"query length {int(queries.shape[1])} != dim {index.dim}")
-    nq = int(queries.shape[0])
+            err = (-1, "query tensors must be contiguous float32")
+    if err is None and index is not None and int(queries.shape[1]) != index.dim:
+        err = (-6, f"query length {int(queries.shape[1])} != dim {index.dim}")
+    nq = int(queries.shape[0]) if queries.ndim >= 1 else 0
+    if err is not None and comm is None:
+        raise BsrError(*err)
     oi = np.empty((nq, top_k), np.uint64)
     od = np.empty((nq, top_k), np.float32)
     oc = np.empty(nq, np.uint32)
-    st = lib().bsr_parallel_top_k_similarity_search(comm._h if comm else None, index._h if index else None,
-                                                    _ptr(queries), nq, top_k, _ptr(oi), _ptr(od), _ptr(oc))
+    # (a rank with an error passes no index: an empty contribution; the batch shape it passes is
+    # still agreed with the others, so a rank whose Q differs makes every rank fail together)
+    st = lib().bsr_parallel_top_k_similarity_search(comm._h if comm else None,
+                                                    index._h if (index and err is None) else None,
+                                                    _ptr(queries) if err is None else None, nq, top_k,
+                                                    _ptr(oi), _ptr(od), _ptr(oc))
+    if err is not None:
+        if rank == ROOT and st == BSR_PARTIAL:
+            warnings.warn(f"{_status_name(err[0])}: {err[1]} (this rank's block is missing from the result)",
+                          RuntimeWarning, stacklevel=2)
+            return oi, od, oc
+        msg = lib().bsr_last_error().decode()
+        extra = "" if st in (BSR_OK, BSR_PARTIAL) or "null index" in msg else f"; the collective: {msg}"
+        raise BsrError(err[0], err[1] + extra)
     _check_parallel(st, rank)
     if rank != ROOT:
         return None

@@ -106,6 +106,22 @@ struct bsr_comm {
     size_t h_mres_bytes = 0;
     uint32_t* h_flag = nullptr;     // fine-grained host word the merge kernel raises
     uint32_t* h_flag_dev = nullptr;
+    // the uncertified queries' staging (parallel_gtau), reserved before the header is posted
+    std::vector<float> f_q, f_dist;
+    std::vector<uint64_t> f_idx;
+    std::vector<uint32_t> f_cnt, f_list;
+    // bsr_comm_init_loopback: one process, every collective emulated on the device (no RCCL).
+    // Without a script each all-gather replicates this rank's contribution P times; with one,
+    // the parallel search's all-gathers replay the recorded contributions of a real P-rank run
+    // (lb_bytes[i] bytes per rank, [P][bytes] at lb_script + lb_off[i]) in their order, this
+    // rank's own slot always live.
+    bool loopback = false;
+    DevBuf lb_script;
+    std::vector<uint64_t> lb_bytes, lb_off;
+    size_t lb_cursor = 0;
+    bool lb_search = false, lb_live = false;
+    int32_t lb_nq = -1, lb_k = -1;  // the recorded search's batch shape (its header): replayed only for it
+    uint64_t lb_replayed = 0, lb_missed = 0;
     ~bsr_comm() {
         if (h_mres) (void)hipHostFree(h_mres);
         if (h_flag) (void)hipHostFree(h_flag);
@@ -136,6 +152,46 @@ constexpr int32_t kHdrMagic = 0x42535231;
         if (r_ != ncclSuccess)                                                                  \
             return set_error(BSR_E_RCCL, "%s failed: %s", #call, ncclGetErrorString(r_));       \
     } while (0)
+
+// One all-gather of `bytes` device bytes per rank on `stream`: RCCL, or the loopback
+// communicator's emulation (one kernel on the same stream, where ncclAllGather would sit).
+static int coll_allgather(bsr_comm* c, const void* send, void* recv, size_t bytes, hipStream_t stream) {
+    if (!c->loopback) {
+        BSR_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c->comm, stream));
+        return BSR_OK;
+    }
+    const void* script = nullptr;
+    if (c->lb_search && c->lb_live && !c->lb_bytes.empty()) {
+        if (c->lb_cursor < c->lb_bytes.size() && c->lb_bytes[c->lb_cursor] == bytes) {
+            script = c->lb_script.as<uint8_t>() + c->lb_off[c->lb_cursor++];
+            ++c->lb_replayed;
+        } else {  // (the recording ends, or another call sequence: replicate from here on)
+            c->lb_live = false;
+            ++c->lb_missed;
+        }
+    }
+    BSR_HIP(launch_gather_emulate(send, script, recv, bytes, (uint32_t)c->size, (uint32_t)c->rank, stream));
+    return BSR_OK;
+}
+static int coll_group(bsr_comm* c, bool start) {
+    if (c->loopback) return BSR_OK;
+    if (start) BSR_NCCL(ncclGroupStart());
+    else BSR_NCCL(ncclGroupEnd());
+    return BSR_OK;
+}
+
+// The parallel search's header buffers, allocated with the communicator: posting a header can
+// then fail only in the transport, which every rank sees.
+constexpr size_t kHdrWordsInit = 8;
+static int alloc_header(bsr_comm* c) {
+    const size_t P = (size_t)c->size, hb = kHdrWordsInit * sizeof(int32_t);
+    BSR_TRY(c->h_hdr.resize(kHdrWordsInit * (1 + P)));
+    if (!c->host_fn) {
+        BSR_TRY(c->hdr_send.ensure(hb));
+        BSR_TRY(c->hdr_recv.ensure(hb * P));
+    }
+    return BSR_OK;
+}
 
 // ---------------------------------------------------------------------------------------
 // C ABI
@@ -319,6 +375,11 @@ static int comm_init_impl(const uint8_t id[BSR_UNIQUE_ID_BYTES], int32_t rank, i
         delete c;
         return set_error(BSR_E_HIP, "hipStreamCreate failed");
     }
+    const int ra = alloc_header(c);
+    if (ra != BSR_OK) {
+        bsr_comm_destroy(c);
+        return ra;
+    }
     *out = c;
     return BSR_OK;
 }
@@ -335,6 +396,11 @@ static int comm_init_host_impl(int32_t rank, int32_t size, bsr_host_allgather_fn
     c->size = size;
     c->host_fn = fn;
     c->host_user = user;
+    const int ra = alloc_header(c);
+    if (ra != BSR_OK) {
+        delete c;
+        return ra;
+    }
     *out = c;
     return BSR_OK;
 }
@@ -343,14 +409,73 @@ int bsr_comm_init_host(int32_t rank, int32_t size, bsr_host_allgather_fn fn, voi
     BSR_GUARD(comm_init_host_impl(rank, size, fn, user, out));
 }
 
+static int comm_init_loopback_impl(int32_t rank, int32_t size, int32_t device, uint32_t n_calls,
+                                   const uint64_t* call_bytes, const void* script, bsr_comm** out) {
+    if (!out || size < 1 || rank < 0 || rank >= size || (n_calls && (!call_bytes || !script)))
+        return set_error(BSR_E_INVALID, "bad argument");
+    *out = nullptr;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n_calls; ++i) {
+        if (call_bytes[i] % 4) return set_error(BSR_E_INVALID, "recorded all-gather %u: bytes %% 4 != 0", i);
+        total += call_bytes[i] * (uint64_t)size;
+    }
+    BSR_TRY(select_device(device));
+    bsr_comm* c = new bsr_comm();
+    (void)hipGetDevice(&c->device);
+    c->rank = rank;
+    c->size = size;
+    c->loopback = true;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
+        delete c;
+        return set_error(BSR_E_HIP, "hipStreamCreate failed");
+    }
+    int r = alloc_header(c);
+    if (r == BSR_OK && n_calls) {
+        r = c->lb_script.ensure(total);
+        if (r == BSR_OK && hipMemcpy(c->lb_script.p, script, total, hipMemcpyHostToDevice) != hipSuccess)
+            r = set_error(BSR_E_HIP, "loopback script upload failed");
+        if (call_bytes[0] == 8 * sizeof(int32_t)) {  // the recorded header: this rank's {n_queries, k, ...}
+            const int32_t* h = static_cast<const int32_t*>(script) + 8 * (size_t)rank;
+            c->lb_nq = h[0];
+            c->lb_k = h[1];
+        }
+        uint64_t off = 0;
+        for (uint32_t i = 0; r == BSR_OK && i < n_calls; ++i) {
+            c->lb_bytes.push_back(call_bytes[i]);
+            c->lb_off.push_back(off);
+            off += call_bytes[i] * (uint64_t)size;
+        }
+    }
+    if (r != BSR_OK) {
+        bsr_comm_destroy(c);
+        return r;
+    }
+    *out = c;
+    return BSR_OK;
+}
+
+int bsr_comm_init_loopback(int32_t rank, int32_t size, int32_t device, uint32_t n_calls, const uint64_t* call_bytes,
+                           const void* script, bsr_comm** out) {
+    BSR_GUARD(comm_init_loopback_impl(rank, size, device, n_calls, call_bytes, script, out));
+}
+
+int bsr_comm_loopback_stats(const bsr_comm* c, uint64_t* replayed, uint64_t* missed) {
+    if (!c || !replayed || !missed) return set_error(BSR_E_INVALID, "null argument");
+    if (!c->loopback) return set_error(BSR_E_INVALID, "not a loopback communicator");
+    *replayed = c->lb_replayed;
+    *missed = c->lb_missed;
+    return BSR_OK;
+}
+
 void bsr_comm_destroy(bsr_comm* c) {
     if (!c) return;
     try {
-        if (c->comm) {
+        if (c->stream) {
             (void)hipSetDevice(c->device);
-            if (c->stream) { (void)hipStreamSynchronize(c->stream); (void)hipStreamDestroy(c->stream); }
-            ncclCommDestroy(c->comm);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamDestroy(c->stream);
         }
+        if (c->comm) ncclCommDestroy(c->comm);
         delete c;
     } catch (...) {}
 }
@@ -428,11 +553,11 @@ static int exchange_lists(bsr_comm* c, const uint64_t* idx, const float* dist, c
     BSR_TRY(c->recv_idx.ensure(nk * P * sizeof(uint64_t)));
     BSR_TRY(c->recv_dist.ensure(nk * P * sizeof(float)));
     BSR_TRY(c->recv_cnt.ensure((size_t)nq * P * sizeof(uint32_t)));
-    BSR_NCCL(ncclGroupStart());
-    BSR_NCCL(ncclAllGather(s_idx, c->recv_idx.p, nk * sizeof(uint64_t), ncclUint8, c->comm, stream));
-    BSR_NCCL(ncclAllGather(s_dist, c->recv_dist.p, nk * sizeof(float), ncclUint8, c->comm, stream));
-    BSR_NCCL(ncclAllGather(s_cnt, c->recv_cnt.p, (size_t)nq * sizeof(uint32_t), ncclUint8, c->comm, stream));
-    BSR_NCCL(ncclGroupEnd());
+    BSR_TRY(coll_group(c, true));
+    BSR_TRY(coll_allgather(c, s_idx, c->recv_idx.p, nk * sizeof(uint64_t), stream));
+    BSR_TRY(coll_allgather(c, s_dist, c->recv_dist.p, nk * sizeof(float), stream));
+    BSR_TRY(coll_allgather(c, s_cnt, c->recv_cnt.p, (size_t)nq * sizeof(uint32_t), stream));
+    BSR_TRY(coll_group(c, false));
     if (!to_host) return BSR_OK;  // the lists stay in recv_* (stream-ordered consumers follow)
     if (root) {
         BSR_TRY(c->h_idx.resize(nk * P));
@@ -568,7 +693,8 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool g
     const size_t P = (size_t)c->size, hb = kHdrWords * sizeof(int32_t);
     if (first && inject_header_fault(c))
         return set_error(BSR_E_NOMEM, "injected fault: header buffers (BSR_INJECT_FAULT)");
-    BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));
+    static_assert(kHdrWords == kHdrWordsInit, "header buffers sized at init");
+    BSR_TRY(c->h_hdr.resize(kHdrWords * (1 + P)));  // (allocated at init: never fails here)
     int32_t* h = c->h_hdr.data();
     h[0] = (int32_t)nq;
     h[1] = (int32_t)k;
@@ -585,10 +711,8 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool g
         return BSR_OK;
     }
     BSR_HIP(hipSetDevice(c->device));
-    BSR_TRY(c->hdr_send.ensure(hb));
-    BSR_TRY(c->hdr_recv.ensure(hb * P));
     BSR_HIP(hipMemcpyAsync(c->hdr_send.p, h, hb, hipMemcpyHostToDevice, c->stream));
-    BSR_NCCL(ncclAllGather(c->hdr_send.p, c->hdr_recv.p, hb, ncclUint8, c->comm, c->stream));
+    BSR_TRY(coll_allgather(c, c->hdr_send.p, c->hdr_recv.p, hb, c->stream));
     c->hdr_posted = true;
     BSR_HIP(hipMemcpyAsync(h + kHdrWords, c->hdr_recv.p, hb * P, hipMemcpyDeviceToHost, c->stream));
     return BSR_OK;
@@ -600,14 +724,21 @@ static int header_wait(bsr_comm* c) {
 static const int32_t* header_of(const bsr_comm* c, int32_t r) {
     return c->h_hdr.data() + kHdrWords * (1 + (size_t)r);
 }
+// Post this search's header exactly once: a first attempt that failed before it was posted (the
+// injected fault; the buffers exist since the communicator was created) is posted again carrying
+// that failure, returned in *local_err.  Returns a transport error, which every rank sees.
+static int post_header(bsr_comm* c, uint32_t nq, uint32_t k, int st, bool gt, uint64_t n, int* local_err) {
+    *local_err = BSR_OK;
+    const int hs = header_start(c, nq, k, st, gt, n, true);
+    if (hs == BSR_OK || c->hdr_posted) return hs;
+    *local_err = hs;
+    return header_start(c, nq, k, st != BSR_OK ? st : hs, false, n);
+}
 
 // An all-gather of `bytes` device bytes per rank on `stream` (RCCL), or through the host
 // transport (staged through pinned memory: a host round trip).
 static int allgather_device(bsr_comm* c, const void* send, void* recv, size_t bytes, hipStream_t stream) {
-    if (!c->host_fn) {
-        BSR_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c->comm, stream));
-        return BSR_OK;
-    }
+    if (!c->host_fn) return coll_allgather(c, send, recv, bytes, stream);
     const size_t P = (size_t)c->size;
     BSR_TRY(c->h_stage.resize(bytes * (1 + P)));
     uint8_t* hs = c->h_stage.data();
@@ -650,6 +781,13 @@ static int gtau_reserve(bsr_comm* c, const bsr_index* ix, uint32_t nq, uint32_t 
     BSR_TRY(c->g_res.ensure(rbytes * P));
     BSR_TRY(c->m_res.ensure(mbytes));
     if (c->host_fn) BSR_TRY(c->h_stage.resize(std::max(kb, rbytes) * (1 + P)));
+    // (the uncertified queries' staging: sized now, so that no allocation can fail between the
+    // merge and the fallback's collectives)
+    c->f_q.reserve((size_t)nq * ix->dim);
+    c->f_idx.reserve((size_t)nq * k);
+    c->f_dist.reserve((size_t)nq * k);
+    c->f_cnt.reserve(nq);
+    c->f_list.reserve(nq);
     if (c->h_mres_bytes < mbytes) {
         if (c->h_mres) BSR_HIP(hipHostFree(c->h_mres));
         c->h_mres = nullptr;
@@ -770,38 +908,46 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     uint32_t* m_cnt = reinterpret_cast<uint32_t*>(hm + o_cnt);
     float* m_dist = reinterpret_cast<float*>(hm + o_dist);
     uint64_t* m_idx = reinterpret_cast<uint64_t*>(hm + o_idx);
+    int fr = BSR_OK;  // the fallback's status (BSR_PARTIAL on a root whose own search failed)
     if (nf) {
-        std::vector<uint32_t> fl(reinterpret_cast<const uint32_t*>(hm + o_fail),
-                                 reinterpret_cast<const uint32_t*>(hm + o_fail) + nf);
+        // (staging reserved by gtau_reserve: these resizes do not allocate.  A local failure
+        // here still takes part in the fallback's collectives -- with no queries, i.e. an empty
+        // contribution -- and is returned after them.)
+        std::vector<uint32_t>& fl = c->f_list;
+        fl.assign(reinterpret_cast<const uint32_t*>(hm + o_fail), reinterpret_cast<const uint32_t*>(hm + o_fail) + nf);
         std::sort(fl.begin(), fl.end());
         const uint32_t d = ix->dim;
-        // (gathered into host memory: nothing is allocated on the device between collectives)
-        std::vector<float> hq((size_t)nf * d);
+        c->f_q.resize((size_t)nf * d);
         const bool qdev = is_device_ptr(queries);
-        for (uint32_t i = 0; i < nf; ++i) {
-            if (qdev)
-                BSR_HIP(hipMemcpyAsync(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float),
-                                       hipMemcpyDeviceToHost, s));
-            else
-                memcpy(hq.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float));
+        int staged = BSR_OK;
+        for (uint32_t i = 0; i < nf && staged == BSR_OK; ++i) {
+            if (!qdev) memcpy(c->f_q.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float));
+            else if (hipMemcpyAsync(c->f_q.data() + (size_t)i * d, queries + (size_t)fl[i] * d, d * sizeof(float),
+                                    hipMemcpyDeviceToHost, s) != hipSuccess)
+                staged = set_error(BSR_E_HIP, "staging the uncertified queries failed");
         }
-        if (qdev) BSR_HIP(stream_wait(s));
-        const float* fq = hq.data();
-        std::vector<uint64_t> fi((size_t)nf * k);
-        std::vector<float> fd((size_t)nf * k);
-        std::vector<uint32_t> fc(nf);
+        if (qdev && staged == BSR_OK && stream_wait(s) != hipSuccess)
+            staged = set_error(BSR_E_HIP, "staging the uncertified queries failed");
+        std::string staged_err = staged == BSR_OK ? std::string() : std::string(last_error_cstr());
+        c->f_idx.resize((size_t)nf * k);
+        c->f_dist.resize((size_t)nf * k);
+        c->f_cnt.resize(nf);
         const bsr_search_stats keep = ix->stats;
-        const int r = parallel_impl(c, ix, fq, nf, k, fi.data(), fd.data(), fc.data(), false);
+        fr = parallel_impl(c, ix, staged == BSR_OK ? c->f_q.data() : nullptr, nf, k, c->f_idx.data(),
+                           c->f_dist.data(), c->f_cnt.data(), false);
         ix->stats.n_emitted = keep.n_emitted;
         ix->stats.n_fallback = nf;
         ix->stats.n_queries = nq;
-        if (r != BSR_OK) return r;
+        if (staged != BSR_OK && !root) return set_error(staged, "%s", staged_err.c_str());
+        // a root whose own fallback search failed still has the other ranks' rows (BSR_PARTIAL):
+        // they are patched in and the merged result is handed out with that status
+        if (fr != BSR_OK && !(root && fr == BSR_PARTIAL)) return fr;
         if (root)
             for (uint32_t i = 0; i < nf; ++i) {
                 const uint32_t q = fl[i];
-                m_cnt[q] = fc[i];
-                memcpy(m_idx + (size_t)q * k, fi.data() + (size_t)i * k, k * sizeof(uint64_t));
-                memcpy(m_dist + (size_t)q * k, fd.data() + (size_t)i * k, k * sizeof(float));
+                m_cnt[q] = c->f_cnt[i];
+                memcpy(m_idx + (size_t)q * k, c->f_idx.data() + (size_t)i * k, k * sizeof(uint64_t));
+                memcpy(m_dist + (size_t)q * k, c->f_dist.data() + (size_t)i * k, k * sizeof(float));
             }
     }
     if (!root) return clear_counts(out_count, nq);
@@ -814,7 +960,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         memcpy(out_dist, m_dist, nqk * sizeof(float));
         memcpy(out_count, m_cnt, (size_t)nq * sizeof(uint32_t));
     }
-    return BSR_OK;
+    return fr;  // (BSR_OK, or BSR_PARTIAL with bsr_last_error() from the fallback)
 }
 
 // parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206).  Collective-safe:
@@ -858,26 +1004,45 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
             else if (gtau_reserve(c, ix, nq, k) != BSR_OK) gt = false;  // (the standard path then)
         }
         c->hdr_posted = false;
-        const int hs = header_start(c, nq, k, st, gt, ix ? ix->n : 0, true);
-        if (hs != BSR_OK && c->hdr_posted) return hs;  // (a transport error: every rank sees it)
-        if (!c->hdr_posted) {  // not posted: post it once more, carrying this failure
-            if (st == BSR_OK) st = hs;
-            gt = false;
-            BSR_TRY(header_start(c, nq, k, st, false, ix ? ix->n : 0));
+        const uint64_t n_rows = ix ? ix->n : 0;
+        int lerr = BSR_OK;
+        if (gt) {
+            // (phase A is enqueued: the header overlaps it)
+            BSR_TRY(post_header(c, nq, k, st, true, n_rows, &lerr));  // (a transport error: every rank sees it)
+            if (lerr != BSR_OK) {  // reposted with the failure: this rank, so every rank, is off the path
+                st = lerr;
+                gt = false;
+            }
         }
         if (!gt) {
-            // this rank is not on the global-threshold path, so no rank is: its standard search
-            // starts now, and the header's wait rides the search's hook (overlapping the search)
-            struct HookCtx { bsr_comm* c; int st; bool ran; } hc{c, BSR_OK, false};
+            // No rank is on the global-threshold path: the standard search starts now and the header
+            // is posted and waited for from the search's hook, after the persistent filter has been
+            // launched (an RCCL kernel waiting for a late peer then cannot hold a CU the filter's
+            // one-workgroup-per-CU grid needs), overlapping the search.
+            struct HookCtx {
+                bsr_comm* c;
+                uint32_t nq, k;
+                uint64_t n;
+                int lerr, hst;
+                bool ran;
+            } hc{c, nq, k, n_rows, BSR_OK, BSR_OK, false};
             auto hook = [](void* p) -> int {
                 HookCtx* h = static_cast<HookCtx*>(p);
                 h->ran = true;
-                h->st = header_wait(h->c);
-                return h->st;
+                if (!h->c->hdr_posted) h->hst = post_header(h->c, h->nq, h->k, BSR_OK, false, h->n, &h->lerr);
+                if (h->hst == BSR_OK) h->hst = header_wait(h->c);
+                return h->hst;
             };
-            if (st == BSR_OK) st = ix->search_device(queries, nq, k, +hook, &hc);
-            if (!hc.ran) hc.st = header_wait(c);  // (the search failed before its launch, or never ran)
-            if (hc.st != BSR_OK) return hc.st;   // (a transport error: every rank sees it)
+            if (st == BSR_OK) {
+                st = ix->search_device(queries, nq, k, +hook, &hc);
+                if (hc.ran && hc.hst != BSR_OK) return hc.hst;  // (a transport error: every rank sees it)
+                if (st == BSR_OK && hc.lerr != BSR_OK) st = hc.lerr;  // (an empty contribution, then this error)
+            }
+            if (!c->hdr_posted) {  // the search failed before its launch, or never ran
+                BSR_TRY(post_header(c, nq, k, st, false, n_rows, &lerr));
+                if (st == BSR_OK) st = lerr;
+            }
+            if (!hc.ran) BSR_TRY(header_wait(c));
             searched = true;
         } else {
             BSR_TRY(header_wait(c));
@@ -951,9 +1116,21 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     return set_error(st, "%s", local_err.c_str());
 }
 
+static int parallel_top(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k, uint64_t* out_idx,
+                        float* out_dist, uint32_t* out_count) {
+    if (c && c->loopback) {  // a loopback script replays the recorded search's all-gathers, from its first
+        c->lb_search = true;
+        c->lb_live = c->lb_nq == (int32_t)nq && c->lb_k == (int32_t)k;  // (another batch shape: replicate)
+        c->lb_cursor = 0;
+    }
+    const int r = parallel_impl(c, ix, queries, nq, k, out_idx, out_dist, out_count, true);
+    if (c) c->lb_search = false;
+    return r;
+}
+
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries, uint32_t n_queries,
                                          uint32_t k, uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
-    BSR_GUARD(parallel_impl(comm, ix, queries, n_queries, k, out_idx, out_dist, out_count, true));
+    BSR_GUARD(parallel_top(comm, ix, queries, n_queries, k, out_idx, out_dist, out_count));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -977,7 +1154,7 @@ static int allgather_bytes_impl(bsr_comm* c, const void* send, void* recv, uint6
     BSR_TRY(ds.ensure(bytes));
     BSR_TRY(dr.ensure(bytes * P));
     BSR_HIP(hipMemcpyAsync(ds.p, send, bytes, hipMemcpyDefault, c->stream));
-    BSR_NCCL(ncclAllGather(ds.p, dr.p, bytes, ncclUint8, c->comm, c->stream));
+    BSR_TRY(coll_allgather(c, ds.p, dr.p, bytes, c->stream));
     BSR_HIP(hipMemcpyAsync(recv, dr.p, bytes * P, hipMemcpyDefault, c->stream));
     BSR_HIP(hipStreamSynchronize(c->stream));
     return BSR_OK;
@@ -998,6 +1175,7 @@ static int broadcast_impl(bsr_comm* c, void* buf, uint64_t bytes, int32_t root) 
         BSR_HIP_OR_HOST_COPY(buf, hr.data() + (size_t)root * bytes, bytes);
         return BSR_OK;
     }
+    if (c->loopback) return BSR_OK;  // (one process: this rank's buffer stands for the root's)
     BSR_HIP(hipSetDevice(c->device));
     void* d = buf;
     DevBuf tmp;

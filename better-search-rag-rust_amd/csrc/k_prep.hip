@@ -11,6 +11,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace bsr {
 
 // ------------------------------------------------------------------------------------
@@ -426,6 +428,25 @@ static inline uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap = 65
     return (uint32_t)(g > cap ? cap : g);
 }
 
+// ------------------------------------------------------------------------------------
+// The loopback communicator's all-gather (bsr_comm_init_loopback): slot r of
+// recv [P][bytes] receives this rank's `send` (r == rank, or every slot when there is no
+// script) or the recorded contribution script[r] of a real P-rank run -- one launch on the
+// stream where ncclAllGather would sit, no host wait.  bytes % 4 == 0.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gather_emulate(const uint32_t* __restrict__ send,
+                                                        const uint32_t* __restrict__ script,
+                                                        uint32_t* __restrict__ recv, uint64_t words,
+                                                        uint32_t P, uint32_t rank) {
+    const uint64_t total = words * P;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(e / words);
+        const uint64_t i = e - (uint64_t)r * words;
+        recv[e] = (script && r != rank) ? script[e] : send[i];
+    }
+}
+
 hipError_t launch_synth_uniform(float* out, uint64_t row0, uint64_t n_rows, uint32_t dim,
                                 uint32_t ld, uint64_t seed, hipStream_t s) {
     hipLaunchKernelGGL(k_synth_uniform, dim3(grid_for(n_rows * ld, 256)), dim3(256), 0, s, out, row0,
@@ -467,6 +488,16 @@ hipError_t launch_rows_to_i8_sample(const float* rows, uint64_t n, uint32_t dim,
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_query_prep, dim3(a.qpad), dim3(128), 0, s, a.q, a.nq, a.dim, a.ld, a.with_op,
                        a.ea_max, a.qf32, a.nb, a.qop, a.qscale, a.ebound, a.qflags, a.qids, a.status);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_emulate(const void* send, const void* script, void* recv, uint64_t bytes, uint32_t P,
+                                 uint32_t rank, hipStream_t s) {
+    if (bytes % 4) return hipErrorInvalidValue;
+    const uint64_t words = bytes / 4, total = words * P;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (total + 255) / 256));
+    hipLaunchKernelGGL(k_gather_emulate, dim3(grid), dim3(256), 0, s, static_cast<const uint32_t*>(send),
+                       static_cast<const uint32_t*>(script), static_cast<uint32_t*>(recv), words, P, rank);
     return hipGetLastError();
 }
 

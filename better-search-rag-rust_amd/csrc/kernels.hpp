@@ -66,6 +66,10 @@ struct QueryPrepArgs {
     bool with_op;          // build the filter operand (false: exact scan only)
 };
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s);
+// The loopback communicator's all-gather: recv[r] = script[r] (a recorded contribution of a real
+// P-rank run) for r != rank, this rank's send otherwise (every slot when script is null).
+hipError_t launch_gather_emulate(const void* send, const void* script, void* recv, uint64_t bytes, uint32_t P,
+                                 uint32_t rank, hipStream_t s);
 
 // ---- MFMA candidate filter (k_filter.hip) ---------------------------------------------
 struct GemmArgs {

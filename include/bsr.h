@@ -90,7 +90,7 @@ typedef struct {
 } bsr_rank_interval;
 
 typedef struct bsr_index bsr_index; /* one rank's corpus shard, resident in HBM */
-typedef struct bsr_comm bsr_comm;   /* RCCL communicator over the ranks (one GPU each) */
+typedef struct bsr_comm bsr_comm;   /* the rank group: RCCL (one GPU each), a host transport or a loopback */
 
 /* Per-search statistics of the last bsr_local_top_k on an index. */
 typedef struct {
@@ -179,6 +179,21 @@ typedef int (*bsr_host_allgather_fn)(const void* send, void* recv, uint64_t byte
 int bsr_comm_init_host(int32_t rank, int32_t size, bsr_host_allgather_fn fn, void* user,
                        bsr_comm** out);
 
+/* Loopback communicator (measurement and tests, not a transport): ONE process on one GPU acting
+ * as rank `rank` of `size`.  Every all-gather is emulated by one device kernel enqueued exactly
+ * where ncclAllGather would be (same stream, no host wait), so a parallel search runs the RCCL
+ * path's enqueue-only control flow and its per-rank device timeline.  Without a script
+ * (n_calls = 0) each all-gather gives every slot this rank's own contribution.  With one, the
+ * all-gathers of each bsr_parallel_top_k_similarity_search replay, in order, the contributions
+ * recorded in a real size-rank run of the same batch (call i: call_bytes[i] bytes per rank,
+ * script holds its [size][call_bytes[i]] receive buffer, calls concatenated); this rank's slot
+ * is always its live contribution, and a call that does not match the recording (another
+ * size, past its end) replicates from then on in that search.  Broadcasts are no-ops. */
+int bsr_comm_init_loopback(int32_t rank, int32_t size, int32_t device, uint32_t n_calls,
+                           const uint64_t* call_bytes, const void* script, bsr_comm** out);
+/* All-gathers replayed from the script and calls that missed it, since creation. */
+int bsr_comm_loopback_stats(const bsr_comm* comm, uint64_t* replayed, uint64_t* missed);
+
 /* ---- a-4: gather_top_k_results.  Every rank passes its [n_queries][k] local lists;
  * the root (rank 0) receives [size][n_queries][k] lists + counts in rank order
  * (host buffers, may be NULL on non-root ranks).  Collective: every rank calls it. ---- */
@@ -195,16 +210,31 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
                             const uint32_t* local_count, uint32_t n_queries, uint32_t k,
                             uint64_t* out_idx, float* out_dist, uint32_t* out_count);
 
-/* ---- a-6: parallel_top_k_similarity_search: local search on this rank's shard,
- * RCCL all-gather of the partial lists (bsr_gather_global_top_k), root merge (on the
- * root's GPU).  Root gets the global top-k in out_*; other ranks get out_count[q] = 0 (the
- * reference's None).  comm may be NULL for a single-rank run (no exchange).
- * Collective-safe: with size > 1 the ranks first all-gather {n_queries, k, local status}
- * (16 bytes); if they disagree on n_queries or k, every rank returns BSR_E_INVALID and no
- * lists are exchanged.  A rank whose local step fails (bad arguments, device mismatch, a
- * failed search) still completes the exchange with an empty list (:185-191): a non-root
- * rank then returns its error; the root returns BSR_PARTIAL with the other ranks' global
- * top-k in out_* (the reference's root still returns Some(..), :199-202). ------------- */
+/* ---- a-6: parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206) for a batch
+ * of n_queries queries.  The root (rank 0) gets the global top-k in out_* (the reference's
+ * Some(global_top_k)); other ranks get out_count[q] = 0 (its None).  comm may be NULL for a
+ * single-rank run (the local lists are the result).  Collective: every rank calls it.
+ *
+ * With size > 1 every rank first all-gathers a 32-byte header {n_queries, k, local status,
+ * magic, eligible for the global threshold, shard rows (2 words), 0}.  Ranks that disagree on
+ * n_queries or k all return BSR_E_INVALID and no lists move.  Then one of two paths, the same
+ * on every rank:
+ *   - the global-threshold path (every rank eligible: n_queries > 16, k <= 200, a shard of
+ *     more rows than one query's candidate list, size <= 64, size * k <= 1024; the library
+ *     setting BSR_GLOBAL_TAU=0 turns it off): every rank all-gathers its best sample keys,
+ *     emits against the threshold the whole corpus's sample selects, rescores every row it
+ *     emitted exactly and all-gathers its packed result (lists, status words, per-query
+ *     exclusion bounds).  EVERY rank merges the gathered lists on its GPU and certifies each
+ *     merged list against every rank's bound; the uncertified queries (usually none) take the
+ *     standard path below, collectively, and replace the root's rows;
+ *   - the standard path: each rank's certified local top-k (bsr_local_top_k), the all-gather
+ *     of the [n_queries][k] lists and the root's merge on its GPU (bsr_gather_global_top_k).
+ * A rank whose local step fails (bad arguments, device mismatch, a failed search) still takes
+ * part in every collective with an empty list (:185-191): a non-root rank then returns its
+ * error; the root returns BSR_PARTIAL with the other ranks' global top-k in out_* (the
+ * reference's root still returns Some(..), :199-202) and the message in bsr_last_error().
+ * Over RCCL every step is enqueued on the device with one host wait at the end; over a host
+ * transport each all-gather is a host round trip. ------------------------------------------ */
 int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const float* queries,
                                          uint32_t n_queries, uint32_t k, uint64_t* out_idx,
                                          float* out_dist, uint32_t* out_count);

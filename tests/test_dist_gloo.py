@@ -193,6 +193,15 @@ def _worker_collective_safety(rank, world, port, out_path):
         st2, msg2 = 0, ""
     except bsr.BsrError as e:
         st2, msg2 = e.status, str(e)
+    # a rank whose queries fail the Python-side checks (here a float64 tensor) still
+    # takes part in the collective -- an empty contribution -- and raises afterwards; nobody hangs
+    import torch
+    bad_q = torch.zeros((4, D), dtype=torch.float64) if rank == 1 else q
+    try:
+        bsr.parallel_top_k_similarity_search_batch(comm, None, bad_q, K)
+        st3, msg3 = 0, ""
+    except bsr.BsrError as e:
+        st3, msg3 = e.status, str(e)
     # gather_global_top_k: a malformed local list on one rank, then a batch size
     # that differs on one rank -- every rank raises, before any list moves
     li = np.zeros((4, K), np.uint64)
@@ -208,6 +217,7 @@ def _worker_collective_safety(rank, world, port, out_path):
             msgs.append(str(e))
     dist.barrier()
     np.savez(f"{out_path}.{rank}.npz", st=st, st2=st2, msg2=np.frombuffer((msg2 or " ").encode(), np.uint8),
+             st3=st3, msg3=np.frombuffer((msg3 or " ").encode(), np.uint8),
              g1=np.frombuffer((msgs[0] or " ").encode(), np.uint8),
              g2=np.frombuffer((msgs[1] or " ").encode(), np.uint8),
              warned=np.frombuffer((warned or " ").encode(), np.uint8),
@@ -230,6 +240,11 @@ def test_gloo_parallel_search_collective_safety(tmp_path):
     # batch sizes that disagree: all ranks rejected, collectively
     for i in range(world):
         assert int(r[i]["st2"]) == -1 and b"disagree on the batch shape" in r[i]["msg2"].tobytes()
+    # rank 1's float64 queries: it raises its own check's error after the collective; the others
+    # completed it (no index anywhere here: rank 2 reports its null index, the root its partial result)
+    assert int(r[1]["st3"]) == -1 and b"contiguous float32" in r[1]["msg3"].tobytes()
+    assert int(r[0]["st3"]) == 0
+    assert int(r[2]["st3"]) == -1 and b"null index" in r[2]["msg3"].tobytes()
     # gather_global_top_k: malformed lists on rank 1, then Q = 3 on the last rank: all raise
     for i in range(world):
         g1, g2 = r[i]["g1"].tobytes(), r[i]["g2"].tobytes()
