@@ -703,6 +703,10 @@ def main():
                     "emitted per rank), so exchange_ms_per_step understates the all-gathers + merge"
                     if not st.n_candidates else "")),
             "kernels_ms_per_step_rank0": {  # separate profiled pass of n_stage steps (every stage evented)
+                "note": "a separate profiled pass after the timed region (direct launches, HIP events around "
+                        "every stage, a D2H copy and stream wait per search): NOT the timed path, whose "
+                        "ms_per_step replays a captured graph without events; local_search_total can exceed "
+                        "ms_per_step",
                 "filter_emit": round(prof_st.gemm_emit_ms / n_stage, 4),
                 "filter_sample": round(prof_st.gemm_sample_ms / n_stage, 4),
                 "select": round(prof_st.select_ms / n_stage, 4),

@@ -936,6 +936,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         fr = parallel_impl(c, ix, staged == BSR_OK ? c->f_q.data() : nullptr, nf, k, c->f_idx.data(),
                            c->f_dist.data(), c->f_cnt.data(), false);
         ix->stats.n_emitted = keep.n_emitted;
+        ix->stats.n_candidates = 0;  // (this search's path: every emitted row rescored)
         ix->stats.n_fallback = nf;
         ix->stats.n_queries = nq;
         if (staged != BSR_OK && !root) return set_error(staged, "%s", staged_err.c_str());

@@ -12,7 +12,20 @@
 #include <algorithm>
 #include <type_traits>
 
+// Workgroups that write result rows straight into the pinned host mirror (host_put) release them
+// at system scope before they end or arrive at the publish ticket (round 5, VERDICT r04: the
+// memory model's form for a host consumer; 0 = the round-4 form, vmcnt(0) alone -- lab A/B only).
+#ifndef BSR_PUB_SYSREL
+#define BSR_PUB_SYSREL 1
+#endif
+
 namespace {
+// A system-scope release of this wave's prior stores (buffer_wbl2 sc0 sc1 + the wait), then the
+// explicit vmcnt(0) the guide's compiler-hazard note asks for between a release and a flag.
+__device__ __forceinline__ void release_system() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 // The publish copy (device result -> fine-grained host memory) by the threads t of n of one
 // workgroup: 8 loads in flight per thread before their stores (a load-store pair per trip would
 // wait out one load latency per 16 bytes x n)
@@ -156,6 +169,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     // (block 0) or a failure list entry
     __shared__ uint32_t s_wrote;
     if (threadIdx.x == 0) s_wrote = blockIdx.x == 0 ? 1u : 0u;
+    bool host_rows = false;  // (wave 0) this workgroup wrote result rows into the host mirror
     if ((W > 1 || a.excl_out) && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
         // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
         if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
@@ -446,6 +460,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                         if (a.hres_idx) {
                             host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
                             host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
+                            host_rows = true;
                         }
                     }
                 }
@@ -453,22 +468,28 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
                     a.res_cnt[q] = cnt;
                     if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
                 }
+                host_rows = host_rows || a.hres_cnt != nullptr;
             }
         }
         BSR_STAMP(W, 4);
     }
+    // (a kernel that does not publish -- the first pass -- releases its host rows here: the host
+    // reads them once the batch's last kernel has raised the flag)
+    if (BSR_PUB_SYSREL && !a.pub_flag && __ballot(host_rows)) release_system();
     if (a.pub_flag) {
         // publish: every workgroup's writes released (system scope when it wrote result rows
         // to the host mirror itself, else agent scope) before its ticket; the last one acquires
         // them, copies pub_bytes of the packed result (with a host mirror: the status words
         // alone) to host memory, releases it at system scope and raises the flag the host polls
-        // Only a workgroup that wrote what the last one reads releases it (an agent fence writes
-        // back its XCD's L2): block 0's status words, a failure entry -- and, without a host
-        // mirror, the result rows it wrote.  The others only wait for their own host stores
-        // (system scope: complete at vmcnt(0)) before their ticket.
+        // Only a workgroup that wrote what the last one reads releases it to the agent (an agent
+        // fence writes back its XCD's L2): block 0's status words, a failure entry -- and, without
+        // a host mirror, the result rows it wrote.  A workgroup that wrote result rows into the host
+        // mirror releases them at system scope (BSR_PUB_SYSREL) before its ticket: the host reads
+        // them once it sees the flag.
         __shared__ uint32_t s_last;
         __syncthreads();  // (s_wrote final)
         if (s_wrote || (!a.hres_idx && blockIdx.x < n_items)) __threadfence();
+        if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();  // (wave 0 wrote them)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
@@ -846,10 +867,12 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         // mirror of the rows: the part before them) to host memory and raises the host's flag
         // Only a wave that wrote what the last one copies releases it (an agent fence writes back
         // its XCD's L2); the rows count when no host mirror takes them and the copy covers them.
-        // The others only wait for their own host stores (system scope) before their ticket.
+        // A wave whose merged rows went into the host mirror releases them at system scope
+        // (BSR_PUB_SYSREL) before its ticket.
         __shared__ uint32_t s_last;
         const bool rows_copied = !a.hout_idx && a.pub_src + a.pub_bytes > reinterpret_cast<const uint8_t*>(out_count);
         if (wrote || rows_copied) __threadfence();
+        if (BSR_PUB_SYSREL && a.hout_idx && q < nq) release_system();  // (its merged rows, in the host mirror)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (lane == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
@@ -890,16 +913,22 @@ extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rescore_stamps), (size_t)n * 8 * sizeof(uint64_t));
 }
 #endif
+// Chunks of candidate rows in flight in the global-threshold search's rescore of every emitted
+// row (one wave per query, ~32 rows per query per rank at N = 8: latency-bound, not HBM-bound).
+#ifndef BSR_GT_RESCORE_P
+#define BSR_GT_RESCORE_P 2
+#endif
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     if (!a.n_items) return hipSuccess;
     const uint32_t e = (a.k + 63) / 64;
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
     const bool dev = a.n_items_dev != nullptr;
     const dim3 g(dev ? std::min<uint32_t>(a.n_items, kRescoreAllGrid) : a.n_items), b(dev ? 512 : 64);
-#define BSR_RESCORE(E)                                                              \
-    do {                                                                            \
-        if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);           \
-        else hipLaunchKernelGGL((k_rescore<E, 1, 2>), g, b, 0, s, a);               \
+#define BSR_RESCORE(E)                                                                        \
+    do {                                                                                      \
+        if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);                     \
+        else if (a.excl_out) hipLaunchKernelGGL((k_rescore<E, 1, BSR_GT_RESCORE_P>), g, b, 0, s, a); \
+        else hipLaunchKernelGGL((k_rescore<E, 1, 2>), g, b, 0, s, a);                         \
     } while (0)
     switch (e) {
         case 1: BSR_RESCORE(1); break;

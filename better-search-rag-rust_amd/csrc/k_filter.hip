@@ -533,7 +533,9 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 // the 1.25M-row shard, 4% slower at tau = inf, even at 10M (profiles/r04b_fab_*.txt): not kept.
 // TAILX: the dynamic tail in 8 XCD-local pools (the product, tail = 1/8); 0 = one counter per
 // query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
-template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0>
+// L2, FW (lab, round 5): level 2's passing row blocks as a bool array (1) instead of a bit mask
+// (0); FW = 0: no explicit vmcnt(0) in the flush path.
+template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0, int L2 = 0, int FW = 1>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
     // EPI = 3 (lab, stagger): only waves 4-7 -- the SIMD partners of waves 0-3 -- defer their
@@ -676,7 +678,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
         // vmcnt(0) as the builtin (not asm), so that the compiler's wait counting sees the
         // atomic's return complete on this path: otherwise every join after a flush branch
         // (each level-2 append) carries a vmcnt(0) that drains the whole DMA stream
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        if constexpr (FW) __builtin_amdgcn_s_waitcnt(0x0F70);
     };
 
     // STAGE: emission balanced over the workgroup's waves.  A wave whose tile passes level 1
@@ -1122,15 +1124,17 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                     if (!__ballot(((float)mrb[nb] * (mrb[nb] >= 0 ? sc_hi : sc_lo)) * sbq[nb] >= tau[nb])) continue;
                     BSR_FCNT(2);
                     uint32_t pm = 0;  // the lane's passing row blocks
+                    bool pass_rb[8];
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
                         const i32x4v_t& x = acc[rb][nb];
                         const int bm = max(max(x[0], x[1]), max(x[2], x[3]));
-                        pm |= (((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb]) ? 1u << rb : 0u;
+                        if constexpr (L2) pass_rb[rb] = ((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb];
+                        else pm |= (((float)bm * sc[rb >> 1]) * sbq[nb] >= tau[nb]) ? 1u << rb : 0u;
                     }
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
-                        if (!__ballot((pm >> rb) & 1u)) continue;
+                        if (!__ballot(L2 ? pass_rb[rb] : ((pm >> rb) & 1u))) continue;
                         BSR_FCNT(3);
                         if (__ballot(ecnt[nb] > (uint32_t)(CAP - 4))) {  // room for 4 rows (rarely not)
                             flush_ring(nb);
@@ -1512,11 +1516,21 @@ __global__ __launch_bounds__(256) void k_global_tau(const uint64_t* __restrict__
     WaveTopK<E> L;
     L.init();
     uint64_t thr = kKeyNone;
-    for (uint32_t r = 0; r < P; ++r)
-        for (uint32_t b = 0; b < ks; b += kWave) {
-            const uint32_t j = b + lane;
-            L.offer(j < ks ? g[((uint64_t)r * qpad + q) * ks + j] : kKeyNone, (int)ks, thr);
+    // the P * ks keys as one flat sequence, 64 per offer (P = 8, ks = 8: one offer, not eight);
+    // all of a lane's loads are issued before the first offer
+    const uint32_t tot = P * ks;
+    constexpr int NB = 8;
+    for (uint32_t b = 0; b < tot; b += NB * kWave) {
+        uint64_t x[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const uint32_t f = b + u * kWave + lane, r = f / ks, i = f - r * ks;
+            x[u] = f < tot ? g[((uint64_t)r * qpad + q) * ks + i] : kKeyNone;
         }
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            if (b + u * kWave < tot) L.offer(x[u], (int)ks, thr);
+    }
     // (fewer than ks sample keys in the whole corpus: every row is emitted)
     if (lane == 0) tau[q] = thr == kKeyNone ? -INFINITY : score_key_score(thr);
 }
@@ -1609,11 +1623,26 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 // int8 rows of an even number of 64-byte slices up to 12 (dims <= 768): the query-stationary
 // kernel; other widths: k_filter.  (A one-wave-per-SIMD variant
 // with 64 queries per wave, tools/microbench/k_qs64_lab.hip, measured slower: DESIGN.md §5.)
+// Whether any workgroup of the emit filter can run in a row-stream gang (k_filter_qs16's `gang`
+// condition with its longest static stream): otherwise the launch takes the GANG = 0 build, which
+// carries none of the gang code -- 1-2% faster at the small shards of an 8-GPU split and at
+// configs[4]'s 16 query tiles (tools/microbench/filter_hist, profiles/r05c_hist_*).
+static bool gang_possible(const GemmArgs& a, uint32_t grid) {
+    if (!a.tail || a.n_qt < 2 || a.n_qt > 4) return false;
+    const uint32_t G = (grid / 8) / a.n_qt, RG = 8 * G;
+    const uint32_t n_rt = (a.n_rows + 127) / 128, n_st = n_rt - n_rt / 8;  // (TAILX = 8)
+    return RG && n_st && (n_st - 1) / RG + 1 >= kGangMinTiles;
+}
+
 template <bool EMIT>
 static void launch_filter(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB, grid = filter_grid(a.n_qt);
     if (nk % 2 == 0 && nk <= 12) {
         const dim3 g(grid), b(512);
+        if (EMIT && nk == 12 && !gang_possible(a, grid)) {
+            BSR_KLAUNCH((k_filter_qs16<EMIT, 12, 0, 8, 0>), g, b, s, e0, e1, a);
+            return;
+        }
         switch (nk) {
             case 2: BSR_KLAUNCH((k_filter_qs16<EMIT, 2>), g, b, s, e0, e1, a); return;
             case 4: BSR_KLAUNCH((k_filter_qs16<EMIT, 4>), g, b, s, e0, e1, a); return;

@@ -199,6 +199,9 @@ def test_loopback_replicated_matches_own_shard(bsr_mod, oracle_mod, gpu, corpus)
     got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
     st = ix.last_stats()
     assert st.n_candidates == 0  # the global-threshold path (every emitted row rescored)
+    # (replicated contributions: the union is this rank's ~1/8-size emission, so many merged lists
+    # fail certification and take the collective fallback -- exact either way)
+    print(f"loopback (replicated, P = 8): {st.n_fallback} of {len(q)} queries through the fallback")
     _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, _want(oracle_mod, rows, q))
     again = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
     assert all(np.array_equal(a, b) for a, b in zip(got, again))

@@ -21,6 +21,15 @@
 #   fabshard    filter_ab at the rank shards of N = 2, 4, 8 (5M, 2.5M, 1.25M rows) at the global threshold's
 #               emission rate (tau 0.1473: ~256 rows per query over the 10M corpus, 256/N per rank)
 #   fabpmc      FETCH_SIZE of each filter_ab variant at 10M and 1.25M (HBM traffic per launch)
+#   hist        tools/microbench/filter_hist (the product vs the emit filter at earlier commits) at 1M,
+#               1.25M (local-threshold rate) and 1.25M at the global threshold's rate (round 5)
+#   loopback    bench.py --comm loopback --gpus 8: rank 0's step of an 8-rank run on one GPU (the all-gathers
+#               emulated where ncclAllGather sits, replayed from a recorded 8-rank host-transport run)
+#   looprec     record an 8-rank host-transport run's all-gathers ($O/loop8.npz) for the loopback steps below
+#   looptl      rocprofv3 kernel trace of the loopback step (replaying looprec) -> per-search timeline
+#   abloop:A,B  the loopback step with alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree)
+#   mpub        tools/microbench/merge_pub with and without the host-row writers' system-scope release
+#   mrfull      the full-size 8-rank global-threshold tests (configs[2], configs[4])
 #   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
 #               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard
 TAG=${1:-run}
@@ -102,8 +111,44 @@ for step in $STEPS; do
           -d "$O/rehprof" -o run -- python3 bench.py --gpus 8 --comm host --steps 10 --warmup 2 --verify 0 --no-cpu-baseline \
           --p50-iters 3
       find "$O/rehprof" -name "*kernel_stats.csv" | head -3 ;;
+    hist)
+      run 200 "filter_hist 1M" "$O/hist_1m.txt" tools/microbench/filter_hist 1000000 1000 25 0.1253
+      run 200 "filter_hist 1.25M" "$O/hist_125.txt" tools/microbench/filter_hist 1250000 1000 25 0.1284
+      run 200 "filter_hist 1.25M gtau" "$O/hist_125g.txt" tools/microbench/filter_hist 1250000 1000 25 0.1462
+      run 300 "filter_hist 10M" "$O/hist_10m.txt" tools/microbench/filter_hist 10000000 1000 9 0.1473
+      grep -h -E "median|DIFFER" "$O"/hist_*.txt ;;
+    loopback)
+      run 600 "loopback N=8" "$O/bench_loop8.json" python bench.py --comm loopback --gpus 8 --steps 50 --warmup 5 \
+          --verify 4 --no-cpu-baseline
+      head -c 700 "$O/bench_loop8.json"; echo ;;
+    looprec)
+      run 600 "loopback record" "$O/loop_rec.json" python bench.py --comm host --gpus 8 --record-gathers "$O/loop8.npz" \
+          --record-only --settle-ms 0 --warmup 0 --steps 1
+      cat "$O/loop_rec.json" ;;
+    abloop:*)
+      for r in 1 2; do
+        for v in $(echo "${step#*:}" | tr , ' '); do
+          if [ "$v" = new ]; then L=""; else L="tools/ab/libbsr_$v.so"; fi
+          BSR_LIB=$L run 300 "abloop $v $r" "$O/abloop_${v}_$r.json" python bench.py --comm loopback --gpus 8 \
+              --replay "$O/loop8.npz" --steps 50 --warmup 5 --verify 0 --p50-iters 5 $NOB
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_ms_per_step_rank0']; print(sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['emitted_per_query_rank0'], k['rescore'], d['loopback']['missed_allgathers'])" \
+              "$O/abloop_${v}_$r.json" "$v"
+        done
+      done ;;
+    looptl)
+      run 300 "loopback trace" "$O/bench_loop8_prof.json" rocprofv3 --kernel-trace --output-format csv -d "$O/tlloop" -o run -- \
+          python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 $NOB
+      f=$(find "$O/tlloop" -name "*kernel_trace.csv" | head -1)
+      python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_loop8.txt"; tail -30 "$O/timeline_loop8.txt" ;;
+    mpub)
+      run 120 "merge_pub" "$O/merge_pub.txt" tools/microbench/merge_pub 300
+      run 120 "merge_pub no sysrel" "$O/merge_pub_nosysrel.txt" tools/microbench/merge_pub_nosysrel 300
+      cat "$O/merge_pub.txt" "$O/merge_pub_nosysrel.txt" ;;
+    mrfull)
+      timeout -k 10 1500 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k full_size --timeout 900 --timeout-method thread > "$O/pytest_mrfull.log" 2>&1
+      rc=$?; echo "pytest mrfull rc=$rc"; grep -E "emitted per query|PASS|FAIL|Error|passed|failed" "$O/pytest_mrfull.log" | tail -12; [ $rc -eq 0 ] || exit $rc ;;
     mr)
-      timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 200 --timeout-method thread > "$O/pytest_mr.log" 2>&1
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v -k "not full_size" --timeout 200 --timeout-method thread > "$O/pytest_mr.log" 2>&1
       rc=$?; echo "pytest mr rc=$rc"; tail -12 "$O/pytest_mr.log"; [ $rc -eq 0 ] || exit $rc ;;
     stamps)
       for rows in 10000000 1250000; do

@@ -13,6 +13,7 @@
 #include "old/gangs/k_filter.hip"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -85,17 +86,33 @@ int main(int argc, char** argv) {
     const auto g_xp = as_old<bsr_xpools::GemmArgs>(g);
     const auto g_gang = as_old<bsr_gangs::GemmArgs>(g);
     const dim3 G(grid), B(512);
+    // FOCUS=1 (default): the product against its round-5 candidates and the two fastest earlier
+    // kernels; FOCUS=0: every commit of the history as well
+    const bool focus = getenv("FOCUS") == nullptr || atoi(getenv("FOCUS")) != 0;
     std::vector<V> vs = {
         {"product", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12>), G, B, 0, 0, g); }, {}},
-        {"r02", [&] { hipLaunchKernelGGL((bsr_r02::k_filter_qs16<true, 12>), G, B, 0, 0, g_r02); }, {}},
         {"static", [&] { hipLaunchKernelGGL((bsr_static::k_filter_qs16<true, 12>), G, B, 0, 0, g_static); }, {}},
         {"dyntail", [&] { hipLaunchKernelGGL((bsr_dyntail::k_filter_qs16<true, 12>), G, B, 0, 0, g_dyn); }, {}},
-        {"r03", [&] { hipLaunchKernelGGL((bsr_r03::k_filter_qs16<true, 12>), G, B, 0, 0, g_r03); }, {}},
-        {"xpools", [&] { hipLaunchKernelGGL((bsr_xpools::k_filter_qs16<true, 12>), G, B, 0, 0, g_xp); }, {}},
-        {"gangs", [&] { hipLaunchKernelGGL((bsr_gangs::k_filter_qs16<true, 12>), G, B, 0, 0, g_gang); }, {}},
-        {"prod_notail", [&] { bsr::GemmArgs h = g; h.tail = nullptr;
-                              hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12>), G, B, 0, 0, h); }, {}},
+        // round-5 variants of the product: GANG = 0 (no gang code compiled), TAILX = 0 (one tail
+        // counter per query tile), L2 = 1 (level 2's bool-array form), FW = 0 (no explicit wait
+        // in the flush)
+        {"g0_l2b_fw0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 8, 0, 0, 1, 0>), G, B, 0, 0, g); }, {}},
+        {"g0_t0_l2b_fw0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 0, 0, 0, 1, 0>), G, B, 0, 0, g); }, {}},
+        {"g2_l2b_fw0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 8, 2, 0, 1, 0>), G, B, 0, 0, g); }, {}},
     };
+    if (!focus) {
+        std::vector<V> more = {
+            {"r02", [&] { hipLaunchKernelGGL((bsr_r02::k_filter_qs16<true, 12>), G, B, 0, 0, g_r02); }, {}},
+            {"r03", [&] { hipLaunchKernelGGL((bsr_r03::k_filter_qs16<true, 12>), G, B, 0, 0, g_r03); }, {}},
+            {"xpools", [&] { hipLaunchKernelGGL((bsr_xpools::k_filter_qs16<true, 12>), G, B, 0, 0, g_xp); }, {}},
+            {"gangs", [&] { hipLaunchKernelGGL((bsr_gangs::k_filter_qs16<true, 12>), G, B, 0, 0, g_gang); }, {}},
+            {"g0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 8, 0>), G, B, 0, 0, g); }, {}},
+            {"g0_l2b", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 8, 0, 0, 1>), G, B, 0, 0, g); }, {}},
+            {"g0_fw0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 8, 0, 0, 0, 0>), G, B, 0, 0, g); }, {}},
+            {"g0_t0", [&] { hipLaunchKernelGGL((bsr::k_filter_qs16<true, 12, 0, 0, 0>), G, B, 0, 0, g); }, {}},
+        };
+        vs.insert(vs.end(), more.begin(), more.end());
+    }
 
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
