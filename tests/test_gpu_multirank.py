@@ -162,7 +162,7 @@ def test_global_threshold_full_size_8_ranks(bsr_mod, oracle_mod, gpu, tmp_path, 
     import test_gpu_full_size as fs
     n, nq, k, bf16, plant = mr_worker.PRESETS[case]
     world = 8
-    res = _run(world, case, tmp_path, timeout=900)
+    res = _run(world, case, tmp_path, timeout=480)
     for r in range(world):
         assert int(res[r]["status"]) == 0, res[r]["msg"].tobytes()
         # the global-threshold path reports no k' candidates (every emitted row was rescored)

@@ -26,6 +26,7 @@
 #   loopback    bench.py --comm loopback --gpus 8: rank 0's step of an 8-rank run on one GPU (the all-gathers
 #               emulated where ncclAllGather sits, replayed from a recorded 8-rank host-transport run)
 #   looprec     record an 8-rank host-transport run's all-gathers ($O/loop8.npz) for the loopback steps below
+#   rstamps     phase stamps of the global-threshold rescore (lab-stamps build; after looprec)
 #   looptl      rocprofv3 kernel trace of the loopback step (replaying looprec) -> per-search timeline
 #   abloop:A,B  the loopback step with alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree)
 #   mpub        tools/microbench/merge_pub with and without the host-row writers' system-scope release
@@ -135,6 +136,9 @@ for step in $STEPS; do
               "$O/abloop_${v}_$r.json" "$v"
         done
       done ;;
+    rstamps)
+      BSR_LIB=tools/ab/libbsr_stamps.so run 300 "rescore stamps gtau" "$O/rstamps_gtau.txt" python tools/diag/rescore_stamps_gtau.py "$O/loop8.npz"
+      grep -v amdgpu.ids "$O/rstamps_gtau.txt" ;;
     looptl)
       run 300 "loopback trace" "$O/bench_loop8_prof.json" rocprofv3 --kernel-trace --output-format csv -d "$O/tlloop" -o run -- \
           python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 $NOB
@@ -145,7 +149,7 @@ for step in $STEPS; do
       run 120 "merge_pub no sysrel" "$O/merge_pub_nosysrel.txt" tools/microbench/merge_pub_nosysrel 300
       cat "$O/merge_pub.txt" "$O/merge_pub_nosysrel.txt" ;;
     mrfull)
-      timeout -k 10 1500 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k full_size --timeout 900 --timeout-method thread > "$O/pytest_mrfull.log" 2>&1
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k full_size --timeout 540 --timeout-method thread > "$O/pytest_mrfull.log" 2>&1
       rc=$?; echo "pytest mrfull rc=$rc"; grep -E "emitted per query|PASS|FAIL|Error|passed|failed" "$O/pytest_mrfull.log" | tail -12; [ $rc -eq 0 ] || exit $rc ;;
     mr)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v -k "not full_size" --timeout 200 --timeout-method thread > "$O/pytest_mr.log" 2>&1
