@@ -837,7 +837,9 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // 1. the sample keys of every rank, then phase B
     const size_t kb = (size_t)ix->gt_qpad * ix->gt_ks * sizeof(uint64_t);
     BSR_TRY(allgather_device(c, ix->smax.p, c->g_smax.p, kb, s));
-    BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P));
+    // (phase B's rescore also sets the merge's fail count and NaN word in m_res: two memset
+    // launches fewer on the critical path)
+    BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P, c->m_res.as<uint32_t>()));
     // 2. the packed result buffers
     const size_t rbytes = ix->res_bytes;
     BSR_TRY(allgather_device(c, ix->res[ix->cur].p, c->g_res.p, rbytes, s));
@@ -846,9 +848,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     const MresLayout L = mres_layout(P, nq, k);
     const size_t o_st = L.o_st, o_fail = L.o_fail, o_cnt = L.o_cnt, o_dist = L.o_dist, o_idx = L.o_idx;
     __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
-    uint8_t* md = c->m_res.as<uint8_t>();
-    BSR_HIP(hipMemsetAsync(md, 0, 4, s));         // fail count
-    BSR_HIP(hipMemsetAsync(md + 4, 0xff, 4, s));  // the lowest query with a NaN distance: none
+    uint8_t* md = c->m_res.as<uint8_t>();  // (its fail count and NaN word were set by phase B's rescore)
     const uint8_t* g = c->g_res.as<uint8_t>();
     MergeArgs ma{};
     ma.idx = reinterpret_cast<const uint64_t*>(g + ix->res_off_idx);

@@ -864,7 +864,7 @@ int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
     return BSR_OK;
 }
 
-int bsr_index::gtau_phase_b(const uint64_t* g_smax, uint32_t P) {
+int bsr_index::gtau_phase_b(const uint64_t* g_smax, uint32_t P, uint32_t* merge_words) {
     bsr_index* ix = this;
     const uint32_t nq = gt_nq, k = gt_k, qpad = gt_qpad;
     BSR_HIP(launch_global_tau(g_smax, P, qpad, nq, gt_ks, qflags.as<uint32_t>(), tau.as<float>(), stream));
@@ -898,6 +898,7 @@ int bsr_index::gtau_phase_b(const uint64_t* g_smax, uint32_t P) {
     ra.emit_cnt = cnt.as<uint32_t>();
     ra.cur_status = d_status;
     ra.n_queries = nq;
+    ra.merge_words = merge_words;  // (the merge's two words: no memset launches before it)
     BSR_HIP(launch_rescore(ra, stream));
     ev_end(ix, ev_rescore);
     ev_end(ix, ev_total);  // (the local part: phases A and B, the all-gather between them included)

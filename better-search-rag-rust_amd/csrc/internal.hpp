@@ -147,7 +147,7 @@ struct bsr_index {
     // Both enqueue only (no host wait).  gtau_eligible: the filter path with a sample pass.
     bool gtau_eligible(uint32_t nq, uint32_t k) const;
     int gtau_phase_a(const float* queries, uint32_t nq, uint32_t k);
-    int gtau_phase_b(const uint64_t* g_smax, uint32_t P);
+    int gtau_phase_b(const uint64_t* g_smax, uint32_t P, uint32_t* merge_words = nullptr);
     bsr::DevBuf smax;
     uint32_t gt_nq = 0, gt_k = 0, gt_qpad = 0, gt_ks = 0;
 };

@@ -173,6 +173,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
     if ((W > 1 || a.excl_out) && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
         // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
         if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
+        if (a.merge_words && threadIdx.x < 2) a.merge_words[threadIdx.x] = threadIdx.x ? ~0u : 0u;
         uint32_t sum = 0;
         for (uint32_t q = threadIdx.x; q < a.n_queries; q += kWave) sum += a.emit_cnt[q];
         sum = wave_reduce_u32(sum, [](uint32_t x, uint32_t y) { return x + y; });

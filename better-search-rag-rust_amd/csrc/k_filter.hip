@@ -1624,9 +1624,12 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 // kernel; other widths: k_filter.  (A one-wave-per-SIMD variant
 // with 64 queries per wave, tools/microbench/k_qs64_lab.hip, measured slower: DESIGN.md §5.)
 // Whether any workgroup of the emit filter can run in a row-stream gang (k_filter_qs16's `gang`
-// condition with its longest static stream): otherwise the launch takes the GANG = 0 build, which
-// carries none of the gang code -- 1-2% faster at the small shards of an 8-GPU split and at
-// configs[4]'s 16 query tiles (tools/microbench/filter_hist, profiles/r05c_hist_*).
+// condition with its longest static stream).  Otherwise -- every shard of up to ~2.4M rows at 1000
+// queries, and configs[4]'s 16 query tiles -- the launch takes the small-shard build: no gang code
+// (GANG = 0), one tail counter per query tile (TAILX = 0), level 2's bool-array form (L2 = 1) and
+// no explicit wait in the flush (FW = 0): 3-4% faster than the gang build at 1M and 1.25M rows
+// with emission, the same at tau = inf (tools/microbench/filter_hist, profiles/r05c_hist_*,
+// r05e_hist_*).  At 10M the gang build stays: its HBM traffic is 1.1x the rows instead of 2x.
 static bool gang_possible(const GemmArgs& a, uint32_t grid) {
     if (!a.tail || a.n_qt < 2 || a.n_qt > 4) return false;
     const uint32_t G = (grid / 8) / a.n_qt, RG = 8 * G;
@@ -1640,7 +1643,7 @@ static void launch_filter(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEv
     if (nk % 2 == 0 && nk <= 12) {
         const dim3 g(grid), b(512);
         if (EMIT && nk == 12 && !gang_possible(a, grid)) {
-            BSR_KLAUNCH((k_filter_qs16<EMIT, 12, 0, 8, 0>), g, b, s, e0, e1, a);
+            BSR_KLAUNCH((k_filter_qs16<EMIT, 12, 0, 0, 0, 0, 1, 0>), g, b, s, e0, e1, a);
             return;
         }
         switch (nk) {

@@ -190,6 +190,9 @@ struct RescoreArgs {
     // no row left out can lie (1 - tau0 - E_q - 2.5e-7 rounded down; -inf when nothing can be
     // certified, +inf when every row was a candidate); the root certifies the merged lists.
     float* excl_out;
+    // (optional, block 0) the parallel search merge's two words, set before its launch:
+    // merge_words[0] = 0 (uncertified count), merge_words[1] = ~0 (lowest query with a NaN)
+    uint32_t* merge_words;
     // Publish (optional, the batch's last kernel): the workgroup that finishes last copies
     // pub_bytes of the packed result buffer pub_src to host memory pub_dst (fine-grained pinned)
     // and then sets *pub_flag = 1 with a system-scope release, so the host sees the result

@@ -66,6 +66,22 @@ def test_bench_two_ranks_host_transport(gpu):
     assert sc["indices_equal"] and sc["distance_bits_equal"]
 
 
+def test_bench_loopback_rank_step(gpu):
+    """bench.py --comm loopback --gpus 4: a recorded 4-rank host-transport run of the batch, then ONE
+    process timing rank 0's step with every all-gather emulated on the device and replayed from
+    that recording; its result is the 4-rank run's global top-k (spot-checked over the whole
+    corpus), every all-gather of the timed searches replayed."""
+    d = _bench("--comm", "loopback", "--gpus", "4", "--rows", "400000", "--verify", "2", *QUICK)
+    _common(d, 1)
+    lb = d["loopback"]
+    assert lb["ranks"] == 4 and lb["recorded_calls_per_search"] == 3
+    assert lb["missed_allgathers"] == 0 and lb["replayed_allgathers"] >= 3 * 3
+    assert d["config"]["rows_per_gpu_rank0"] == 100000 and "loopback" in d["config"]["parallelism"]
+    assert d["candidates_per_query"] == 0  # the global-threshold path
+    sc = d["parity_spot_check"]
+    assert sc["rows"] == 400000 and sc["indices_equal"] and sc["distance_bits_equal"]
+
+
 def _failing_run(extra=(), timeout=60):
     """bench.py --gpus 2 with rank 1 failing on purpose (BSR_BENCH_FAIL_RANK): the launcher must
     end rank 0 -- blocked in a collective with the dead rank -- and report, within the time."""

@@ -32,7 +32,8 @@
 #   mpub        tools/microbench/merge_pub with and without the host-row writers' system-scope release
 #   mrfull      the full-size 8-rank global-threshold tests (configs[2], configs[4])
 #   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
-#               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard
+#               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard; abc2 / abc5:
+#               configs[1] (1M x 1000) / the configs[4] shard (6.25M bf16 x 4096, top-100)
 TAG=${1:-run}
 shift
 STEPS=${*:-tests bench}
@@ -180,8 +181,13 @@ for step in $STEPS; do
             tools/microbench/filter_ab $rows 1000 2 0.1473
         python3 tools/microbench/pmc_summary.py "$O/fabpmc_$rows" > "$O/fabpmc_$rows.txt"; grep -A2 "qs16" "$O/fabpmc_$rows.txt"
       done ;;
-    ab:*|ab125:*)
-      extra=""; [ "${step%%:*}" = ab125 ] && extra="--rows 1250000 --steps 50"
+    ab:*|ab125:*|abc2:*|abc5:*)
+      extra=""
+      case "${step%%:*}" in
+        ab125) extra="--rows 1250000 --steps 50" ;;
+        abc2) extra="--config c2 --steps 30" ;;
+        abc5) extra="--config c5 --steps 5 --warmup 2" ;;
+      esac
       for r in 1 2; do
         for v in $(echo "${step#*:}" | tr , ' '); do
           if [ "$v" = new ]; then L=""; else L="tools/ab/libbsr_$v.so"; fi
