@@ -1499,6 +1499,59 @@ __global__ __launch_bounds__(256) void k_select_tau(const float* __restrict__ S,
     }
 }
 
+// The same selection for short sample rows (n_s <= 64 NV values, ks <= 64: every shard of up to
+// ~2M rows at k <= 10, the shards of an 8-GPU split): ONE wave per query, four per workgroup, the
+// whole row in registers -- its lane maxima's ks-th largest as the lower bound, then the offers
+// from the same registers (no second read, no workgroup merge, no barrier).  The selection is
+// exact either way, so tau and the ks best keys are k_select_tau's, bit for bit.
+template <int NV>
+__global__ __launch_bounds__(256) void k_select_tau_w(const float* __restrict__ S, uint32_t s_ld, uint32_t n_s,
+                                                      uint32_t nq, uint32_t qpad, const uint32_t* __restrict__ qflags,
+                                                      uint32_t ks, float* __restrict__ tau, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ status, uint64_t* __restrict__ smax) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int t = threadIdx.x, lane = t & 63;
+    if (blockIdx.x == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
+    if (blockIdx.x == 0)  // the emit filter's tail counters
+        for (uint32_t i = t; i < 8 * kTailCounters + kGangWords; i += blockDim.x) cnt[qpad + i] = 0;
+    if (q >= qpad) return;
+    if (lane == 0) cnt[q] = 0;
+    const bool none = q >= nq || (qflags[q] & kQueryNoApprox);
+    if (smax && (none || n_s < ks))
+        for (uint32_t i = lane; i < ks; i += kWave) smax[(uint64_t)q * ks + i] = kKeyNone;
+    if (none) {
+        if (lane == 0) tau[q] = INFINITY;  // never emits: answered by the exact scan
+        return;
+    }
+    if (n_s < ks) {
+        if (lane == 0) tau[q] = -INFINITY;
+        return;
+    }
+    const float* s = S + (uint64_t)q * s_ld;
+    float v[NV];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint32_t i = j * kWave + lane;
+        v[j] = i < n_s ? s[i] : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) m = fmaxf(m, v[j]);
+    // the ks-th largest lane maximum: ks distinct values reach it, so it bounds the ks-th value
+    const uint64_t sorted = wave_sort64(score_key(m, (uint32_t)lane));
+    const float lb = score_key_score(shfl64(sorted, (int)ks - 1));
+    WaveTopK<1> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint32_t i = j * kWave + lane;
+        if (j * kWave < (int)n_s) L.offer((i < n_s && v[j] >= lb) ? score_key(v[j], i) : kKeyNone, (int)ks, thr);
+    }
+    if (lane == 0) tau[q] = score_key_score(thr);
+    if (smax) L.store(smax + (uint64_t)q * ks, (int)ks);
+}
+
 // The global emission threshold of a parallel search: tau[q] = the ks-th best
 // of the P ranks' ks best sample keys, all-gathered as g[P][qpad][ks] -- the threshold one
 // shard holding every rank's rows would select.  One wave per query, four per workgroup.
@@ -1669,7 +1722,10 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
                              hipStream_t s, uint64_t* smax) {
     if (ks > 2 * kWave) return hipErrorInvalidValue;
-    if (ks > kWave)
+    if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)
+        hipLaunchKernelGGL(k_select_tau_w<32>, dim3(qpad / 4), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
+                           tau, cnt, status, smax);
+    else if (ks > kWave)
         hipLaunchKernelGGL(k_select_tau<2>, dim3(qpad), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks, tau,
                            cnt, status, smax);
     else
