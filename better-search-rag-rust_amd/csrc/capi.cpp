@@ -1000,7 +1000,9 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         bool gt = allow_gtau && gtau_on && st == BSR_OK && nq > kSkinnyMaxQ && ix->gtau_eligible(nq, k) &&
                   device_merge_fits((uint32_t)c->size, k, k);
         if (gt) {
-            const int r = ix->gtau_phase_a(queries, nq, k);  // (enqueued: the header overlaps it)
+            // every buffer of the path sized first: an allocation failure takes this rank (so every
+            // rank) off the path through its header
+            const int r = ix->gtau_prepare(queries, nq, k);
             if (r != BSR_OK) { st = r; gt = false; }
             else if (gtau_reserve(c, ix, nq, k) != BSR_OK) gt = false;  // (the standard path then)
         }
@@ -1008,11 +1010,16 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         const uint64_t n_rows = ix ? ix->n : 0;
         int lerr = BSR_OK;
         if (gt) {
-            // (phase A is enqueued: the header overlaps it)
+            // the header first, then phase A's kernels: its round trip (to the transport and back to
+            // the host, which enqueues phase B when it has it) overlaps phase A instead of following it
             BSR_TRY(post_header(c, nq, k, st, true, n_rows, &lerr));  // (a transport error: every rank sees it)
             if (lerr != BSR_OK) {  // reposted with the failure: this rank, so every rank, is off the path
                 st = lerr;
                 gt = false;
+            } else {
+                // (enqueue only, every buffer sized: a failure here is a device error -- fatal to the
+                // job, as any device error inside a collective is)
+                BSR_TRY(ix->gtau_phase_a(queries));
             }
         }
         if (!gt) {

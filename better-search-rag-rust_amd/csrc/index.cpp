@@ -812,8 +812,12 @@ bool bsr_index::gtau_eligible(uint32_t nq, uint32_t k) const {
     return loaded && nq > 0 && k >= 1 && k <= cfg.max_k && k <= kMaxKForFilter && approx_ok && n > cap_for(k);
 }
 
-int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
-    bsr_index* ix = this;
+// Phase A's buffers (the result buffer of this search, the query and filter scratch, the sample
+// scores, the ks best keys): everything that can fail short of a device error, done before the
+// parallel search posts its header -- which is then posted before phase A's kernels, so that
+// its round trip overlaps them (round 5: posted after them it could finish behind the sample
+// pass and hold the host's enqueue of phase B, +25 us per search in the loopback timeline).
+int bsr_index::gtau_prepare(const float* queries, uint32_t nq, uint32_t k) {
     if (!gtau_eligible(nq, k)) return set_error(BSR_E_STATE, "global-threshold search not applicable");
     if (!queries) return set_error(BSR_E_INVALID, "null queries");
     BSR_HIP(hipSetDevice(device));
@@ -832,9 +836,26 @@ int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
     BSR_TRY(qids_id.ensure((size_t)qpad * sizeof(int32_t)));
     BSR_TRY(keys.ensure((size_t)nq * k * sizeof(uint64_t)));
     BSR_TRY(smax.ensure((size_t)qpad * ks * sizeof(uint64_t)));
+    if (!is_device_ptr(queries)) BSR_TRY(q_in.ensure((size_t)nq * dim * sizeof(float)));
+    BSR_TRY(filter_buffers(this, nq, qpad, k));
+    const uint32_t n_s = (uint32_t)((n + kSampleStride - 1) / kSampleStride);
+    const uint32_t n_rt_s = (n_s + kFilterTile - 1) / kFilterTile;
+    const bool compact = n_s >= 32u * 8u * ks;
+    const uint32_t s_ld = compact ? n_rt_s * (kFilterTile / 32) : n_rt_s * kFilterTile;
+    BSR_TRY(S.ensure((size_t)qpad * s_ld * sizeof(float)));  // (sample_pass's size)
+    gt_nq = nq;
+    gt_k = k;
+    gt_qpad = qpad;
+    gt_ks = ks;
+    return BSR_OK;
+}
+
+// Phase A's work, enqueued (after gtau_prepare sized every buffer: nothing is allocated here).
+int bsr_index::gtau_phase_a(const float* queries) {
+    bsr_index* ix = this;
+    const uint32_t nq = gt_nq, k = gt_k, qpad = gt_qpad;
     const float* qsrc = queries;
     if (!is_device_ptr(queries)) {
-        BSR_TRY(q_in.ensure((size_t)nq * dim * sizeof(float)));
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
         qsrc = q_in.as<float>();
     }
@@ -857,10 +878,6 @@ int bsr_index::gtau_phase_a(const float* queries, uint32_t nq, uint32_t k) {
     qa.with_op = true;
     BSR_HIP(launch_query_prep(qa, stream));
     BSR_TRY(sample_pass(ix, nq, qpad, k, smax.as<uint64_t>()));
-    gt_nq = nq;
-    gt_k = k;
-    gt_qpad = qpad;
-    gt_ks = ks;
     return BSR_OK;
 }
 

@@ -144,9 +144,11 @@ struct bsr_index {
     //   phase B: the global threshold from the gathered keys g[P][qpad][gt_ks], the emit pass
     //            and the exact rescore of EVERY emitted row, its top-k written as the result
     //            rows with the per-query exclusion bound d_x (no local certification).
-    // Both enqueue only (no host wait).  gtau_eligible: the filter path with a sample pass.
+    // Both enqueue only (no host wait); gtau_prepare sizes every buffer of phase A first.
+    // gtau_eligible: the filter path with a sample pass.
     bool gtau_eligible(uint32_t nq, uint32_t k) const;
-    int gtau_phase_a(const float* queries, uint32_t nq, uint32_t k);
+    int gtau_prepare(const float* queries, uint32_t nq, uint32_t k);  // buffers only (before the header)
+    int gtau_phase_a(const float* queries);                            // launches only
     int gtau_phase_b(const uint64_t* g_smax, uint32_t P, uint32_t* merge_words = nullptr);
     bsr::DevBuf smax;
     uint32_t gt_nq = 0, gt_k = 0, gt_qpad = 0, gt_ks = 0;
