@@ -97,6 +97,13 @@ struct bsr_comm {
     DevBuf hdr_send, hdr_recv;     // the parallel search's shape agreement (RCCL)
     PinnedVec<int32_t> h_hdr;      // [1 + size][kHdrWords]: this rank's words, then every rank's
     bool hdr_posted = false;       // this search's header all-gather has been issued
+    // (device transports) the received headers, published by k_header_publish into fine-grained
+    // pinned memory [size][kHdrWords], and the flag it raises to the search's sequence number
+    int32_t* hdr_host = nullptr;
+    int32_t* hdr_host_dev = nullptr;
+    uint32_t* hdr_flag = nullptr;
+    uint32_t* hdr_flag_dev = nullptr;
+    uint32_t hdr_seq = 0;
     // the global-threshold search (parallel_gtau): gathered sample keys, gathered result
     // buffers, the merged result (device and pinned host)
     DevBuf g_smax, g_res, m_res, pub_ticket;
@@ -125,6 +132,8 @@ struct bsr_comm {
     ~bsr_comm() {
         if (h_mres) (void)hipHostFree(h_mres);
         if (h_flag) (void)hipHostFree(h_flag);
+        if (hdr_host) (void)hipHostFree(hdr_host);
+        if (hdr_flag) (void)hipHostFree(hdr_flag);
     }
 };
 
@@ -189,6 +198,11 @@ static int alloc_header(bsr_comm* c) {
     if (!c->host_fn) {
         BSR_TRY(c->hdr_send.ensure(hb));
         BSR_TRY(c->hdr_recv.ensure(hb * P));
+        BSR_HIP(hipHostMalloc((void**)&c->hdr_host, hb * P, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->hdr_host_dev, c->hdr_host, 0));
+        BSR_HIP(hipHostMalloc((void**)&c->hdr_flag, 64, hipHostMallocCoherent));
+        BSR_HIP(hipHostGetDevicePointer((void**)&c->hdr_flag_dev, c->hdr_flag, 0));
+        __atomic_store_n(c->hdr_flag, 0u, __ATOMIC_RELEASE);
     }
     return BSR_OK;
 }
@@ -704,24 +718,42 @@ static int header_start(bsr_comm* c, uint32_t nq, uint32_t k, int32_t st, bool g
     h[5] = (int32_t)(uint32_t)n_rows;
     h[6] = (int32_t)(uint32_t)(n_rows >> 32);
     h[7] = 0;
+    c->hdr_seq = c->hdr_seq + 1 ? c->hdr_seq + 1 : 1;  // (the published flag's value: never 0)
     if (c->host_fn) {
         c->hdr_posted = true;  // (a failing transport fails on every rank)
         if (c->host_fn(h, h + kHdrWords, hb, c->host_user) != 0)
             return set_error(BSR_E_RCCL, "host all-gather callback failed");
         return BSR_OK;
     }
+    // device transports: kernels only (no host copies, which would hold the host until done)
     BSR_HIP(hipSetDevice(c->device));
-    BSR_HIP(hipMemcpyAsync(c->hdr_send.p, h, hb, hipMemcpyHostToDevice, c->stream));
+    BSR_HIP(launch_header_put(h, c->hdr_send.as<int32_t>(), c->stream));
     BSR_TRY(coll_allgather(c, c->hdr_send.p, c->hdr_recv.p, hb, c->stream));
     c->hdr_posted = true;
-    BSR_HIP(hipMemcpyAsync(h + kHdrWords, c->hdr_recv.p, hb * P, hipMemcpyDeviceToHost, c->stream));
+    BSR_HIP(launch_header_publish(c->hdr_recv.as<int32_t>(), (uint32_t)(kHdrWords * P), c->hdr_host_dev,
+                                  c->hdr_flag_dev, c->hdr_seq, c->stream));
     return BSR_OK;
 }
 static int header_wait(bsr_comm* c) {
-    if (!c->host_fn) BSR_HIP(stream_wait(c->stream));
-    return BSR_OK;
+    if (c->host_fn) return BSR_OK;  // (synchronous)
+    // poll the published flag (checking the stream now and then: one that finished or failed
+    // without raising it is an error, never an endless wait)
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(c->hdr_flag, __ATOMIC_ACQUIRE) == c->hdr_seq) return BSR_OK;
+        if ((i & 4095) == 0) {
+            const hipError_t r = hipStreamQuery(c->stream);
+            if (r == hipSuccess) {
+                if (__atomic_load_n(c->hdr_flag, __ATOMIC_ACQUIRE) == c->hdr_seq) return BSR_OK;
+                return set_error(BSR_E_HIP, "the header exchange finished without publishing");
+            }
+            if (r != hipErrorNotReady) BSR_HIP(r);
+        }
+        __builtin_ia32_pause();
+    }
 }
 static const int32_t* header_of(const bsr_comm* c, int32_t r) {
+    // (host transport: c->h_hdr after this rank's words; device transports: the published copy)
+    if (!c->host_fn) return c->hdr_host + kHdrWords * (size_t)r;
     return c->h_hdr.data() + kHdrWords * (1 + (size_t)r);
 }
 // Post this search's header exactly once: a first attempt that failed before it was posted (the

@@ -447,6 +447,29 @@ __global__ __launch_bounds__(256) void k_gather_emulate(const uint32_t* __restri
     }
 }
 
+// ------------------------------------------------------------------------------------
+// The parallel search's header exchange without host copies (round 5): k_header_put writes this
+// rank's 8 words (kernel arguments) into the device send buffer; after the all-gather,
+// k_header_publish copies the P received headers into fine-grained pinned host memory with
+// system-scope stores, releases them at system scope and then stores the search's sequence
+// number into the host flag the host polls.  (Small hipMemcpyAsync copies to and from pinned
+// memory return only when they are done: the header's two copies held the host's enqueue of
+// phase A / phase B for their round trip.)
+// ------------------------------------------------------------------------------------
+struct HeaderWords { int32_t w[8]; };
+__global__ void k_header_put(HeaderWords h, int32_t* __restrict__ dst) {
+    if (threadIdx.x < 8) dst[threadIdx.x] = h.w[threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_header_publish(const int32_t* __restrict__ src, uint32_t words,
+                                                        int32_t* host, uint32_t* host_flag, uint32_t seq) {
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+        __hip_atomic_store(host + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 hipError_t launch_synth_uniform(float* out, uint64_t row0, uint64_t n_rows, uint32_t dim,
                                 uint32_t ld, uint64_t seed, hipStream_t s) {
     hipLaunchKernelGGL(k_synth_uniform, dim3(grid_for(n_rows * ld, 256)), dim3(256), 0, s, out, row0,
@@ -498,6 +521,18 @@ hipError_t launch_gather_emulate(const void* send, const void* script, void* rec
     const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (total + 255) / 256));
     hipLaunchKernelGGL(k_gather_emulate, dim3(grid), dim3(256), 0, s, static_cast<const uint32_t*>(send),
                        static_cast<const uint32_t*>(script), static_cast<uint32_t*>(recv), words, P, rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_header_put(const int32_t w[8], int32_t* dst, hipStream_t s) {
+    HeaderWords h;
+    for (int i = 0; i < 8; ++i) h.w[i] = w[i];
+    hipLaunchKernelGGL(k_header_put, dim3(1), dim3(64), 0, s, h, dst);
+    return hipGetLastError();
+}
+hipError_t launch_header_publish(const int32_t* src, uint32_t words, int32_t* host, uint32_t* host_flag, uint32_t seq,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_header_publish, dim3(1), dim3(256), 0, s, src, words, host, host_flag, seq);
     return hipGetLastError();
 }
 

@@ -66,6 +66,12 @@ struct QueryPrepArgs {
     bool with_op;          // build the filter operand (false: exact scan only)
 };
 hipError_t launch_query_prep(const QueryPrepArgs& a, hipStream_t s);
+// The parallel search's header exchange without host copies: this rank's 8 words into the device
+// send buffer; the P received headers into fine-grained pinned host memory, then host_flag = seq
+// (system-scope release) -- the host polls the flag.
+hipError_t launch_header_put(const int32_t w[8], int32_t* dst, hipStream_t s);
+hipError_t launch_header_publish(const int32_t* src, uint32_t words, int32_t* host, uint32_t* host_flag, uint32_t seq,
+                                 hipStream_t s);
 // The loopback communicator's all-gather: recv[r] = script[r] (a recorded contribution of a real
 // P-rank run) for r != rank, this rank's send otherwise (every slot when script is null).
 hipError_t launch_gather_emulate(const void* send, const void* script, void* recv, uint64_t bytes, uint32_t P,
