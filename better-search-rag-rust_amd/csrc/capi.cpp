@@ -1042,16 +1042,18 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         const uint64_t n_rows = ix ? ix->n : 0;
         int lerr = BSR_OK;
         if (gt) {
-            // the header first, then phase A's kernels: its round trip (to the transport and back to
-            // the host, which enqueues phase B when it has it) overlaps phase A instead of following it
+            // the query prep, then the header, then the rest of phase A: the GPU starts on the prep
+            // while the host issues the header's launches, and the header's round trip (to the
+            // transport and back to the host, which enqueues phase B when it has it) overlaps phase A
+            // instead of following it.  (Enqueue only, every buffer sized: a failure here is a device
+            // error -- fatal to the job, as any device error inside a collective is.)
+            BSR_TRY(ix->gtau_phase_a(queries, 0));
             BSR_TRY(post_header(c, nq, k, st, true, n_rows, &lerr));  // (a transport error: every rank sees it)
             if (lerr != BSR_OK) {  // reposted with the failure: this rank, so every rank, is off the path
                 st = lerr;
                 gt = false;
             } else {
-                // (enqueue only, every buffer sized: a failure here is a device error -- fatal to the
-                // job, as any device error inside a collective is)
-                BSR_TRY(ix->gtau_phase_a(queries));
+                BSR_TRY(ix->gtau_phase_a(queries, 1));
             }
         }
         if (!gt) {

@@ -850,10 +850,16 @@ int bsr_index::gtau_prepare(const float* queries, uint32_t nq, uint32_t k) {
     return BSR_OK;
 }
 
-// Phase A's work, enqueued (after gtau_prepare sized every buffer: nothing is allocated here).
-int bsr_index::gtau_phase_a(const float* queries) {
+// Phase A's work, enqueued (after gtau_prepare sized every buffer: nothing is allocated here), in
+// two parts so that the parallel search can post its header between them: the query prep (the
+// GPU starts on it while the host issues the header's launches), then the sample pass and tau0.
+int bsr_index::gtau_phase_a(const float* queries, int part) {
     bsr_index* ix = this;
     const uint32_t nq = gt_nq, k = gt_k, qpad = gt_qpad;
+    if (part == 1) {
+        BSR_TRY(sample_pass(ix, nq, qpad, k, smax.as<uint64_t>()));
+        return BSR_OK;
+    }
     const float* qsrc = queries;
     if (!is_device_ptr(queries)) {
         BSR_HIP(hipMemcpyAsync(q_in.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, stream));
@@ -877,7 +883,6 @@ int bsr_index::gtau_phase_a(const float* queries) {
     qa.status = d_status;
     qa.with_op = true;
     BSR_HIP(launch_query_prep(qa, stream));
-    BSR_TRY(sample_pass(ix, nq, qpad, k, smax.as<uint64_t>()));
     return BSR_OK;
 }
 

@@ -148,7 +148,7 @@ struct bsr_index {
     // gtau_eligible: the filter path with a sample pass.
     bool gtau_eligible(uint32_t nq, uint32_t k) const;
     int gtau_prepare(const float* queries, uint32_t nq, uint32_t k);  // buffers only (before the header)
-    int gtau_phase_a(const float* queries);                            // launches only
+    int gtau_phase_a(const float* queries, int part);  // launches only: part 0 query prep, 1 sample + tau0
     int gtau_phase_b(const uint64_t* g_smax, uint32_t P, uint32_t* merge_words = nullptr);
     bsr::DevBuf smax;
     uint32_t gt_nq = 0, gt_k = 0, gt_qpad = 0, gt_ks = 0;
