@@ -142,12 +142,13 @@ __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 // (a.n_items_dev), so the launch needs no host round trip.  P chunks of candidate rows are
 // loaded ahead (rows of 768 floats; other widths: 2).
 #ifdef BSR_RESCORE_STAMPS
-// (lab build only: per-wave phase timestamps of the one-wave-per-query rescore, 100 MHz clock)
+// (lab build only: per-wave phase timestamps of the one-wave-per-query rescore, 100 MHz clock,
+// indexed by the item)
 __device__ uint64_t g_rescore_stamps[4096 * 8];
 #define BSR_STAMP(W_, I_)                                                                          \
     do {                                                                                           \
-        if ((W_) == 1 && threadIdx.x == 0 && blockIdx.x < 4096)                                    \
-            g_rescore_stamps[blockIdx.x * 8 + (I_)] = __builtin_amdgcn_s_memrealtime();            \
+        if ((W_) == 1 && (threadIdx.x & 63) == 0 && item < 4096)                                   \
+            g_rescore_stamps[item * 8 + (I_)] = __builtin_amdgcn_s_memrealtime();                  \
     } while (0)
 #else
 #define BSR_STAMP(W_, I_) \
@@ -155,20 +156,26 @@ __device__ uint64_t g_rescore_stamps[4096 * 8];
     } while (0)
 #endif
 
-template <int E, int W, int P>
-__global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
-    BSR_STAMP(W, 0);
+// QPW > 1 (W = 1): QPW independent waves per workgroup, each its own item with its own LDS stage
+// and query copy (round 5).  One-wave workgroups let the dispatcher put two waves of a 1000-item
+// launch on one SIMD while others stay empty: those waves ran ~1.5x long and set the kernel's
+// time (median wave 27 us, kernel 42 us at the 1.25M shard, profiles/r05e_rstamps_gtau.txt); a
+// 4-wave workgroup with 86 KB of LDS is alone on its CU, one wave per SIMD.
+template <int E, int W, int P, int QPW = 1>
+__global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
+    static_assert(QPW == 1 || W == 1, "independent waves per workgroup: one wave per item");
     constexpr int STAGE = 64 * 68;  // 64 rows (stride 68) per wave
     constexpr int QMAX = 1024;      // the whole query in LDS (rows up to 1024 floats)
-    __shared__ __attribute__((aligned(16))) float lds_all[W * STAGE + QMAX];
+    __shared__ __attribute__((aligned(16))) float lds_all[QPW > 1 ? QPW * (STAGE + QMAX) : W * STAGE + QMAX];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float* const lds = lds_all + w * STAGE;
-    float* const ldq_all = lds_all + W * STAGE;
+    float* const lds = lds_all + (QPW > 1 ? w * (STAGE + QMAX) : w * STAGE);
+    float* const ldq_all = QPW > 1 ? lds + STAGE : lds_all + W * STAGE;
     const uint32_t n_items = a.n_items_dev ? *a.n_items_dev : a.n_items;
     // (publish) this workgroup wrote state the publishing workgroup reads: the status words
     // (block 0) or a failure list entry
     __shared__ uint32_t s_wrote;
     if (threadIdx.x == 0) s_wrote = blockIdx.x == 0 ? 1u : 0u;
+    if constexpr (QPW > 1) __syncthreads();  // (before any wave's failure entry sets it)
     bool host_rows = false;  // (wave 0) this workgroup wrote result rows into the host mirror
     if ((W > 1 || a.excl_out) && a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
         // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
@@ -179,7 +186,8 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         sum = wave_reduce_u32(sum, [](uint32_t x, uint32_t y) { return x + y; });
         if (threadIdx.x == 0) a.cur_status[kStEmitted] = sum;
     }
-    for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    for (uint32_t item = blockIdx.x * QPW + (QPW > 1 ? w : 0); item < n_items; item += gridDim.x * QPW) {
+        BSR_STAMP(W, 0);
         const uint32_t q = a.qlist ? a.qlist[item] : item;
         // mode S (a.sel: select the k' candidates here, from the emitted keys), mode B (every
         // emitted candidate) or mode A (the k' selected ones, from k_select_cand)
@@ -210,14 +218,15 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             constexpr int QN = QMAX / (64 * W);
             const float* qsrc = a.qf32 + (uint64_t)q * a.ld;
             float qv[QN];
+            const uint32_t tq = QPW > 1 ? (uint32_t)lane : threadIdx.x;  // (this item's threads)
 #pragma unroll
             for (int j = 0; j < QN; ++j) {
-                const uint32_t cc = j * 64 * W + threadIdx.x;
+                const uint32_t cc = j * 64 * W + tq;
                 qv[j] = cc < a.ld ? qsrc[cc] : 0.0f;
             }
 #pragma unroll
             for (int j = 0; j < QN; ++j) {
-                const uint32_t cc = j * 64 * W + threadIdx.x;
+                const uint32_t cc = j * 64 * W + tq;
                 if (cc < a.ld) ldq_all[cc] = qv[j];
             }
         }
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             constexpr bool QL = decltype(ql_tag)::value;
             constexpr uint32_t NC = decltype(nc_tag)::value;
             const uint32_t nchk = NC ? NC : nch;
-            for (uint32_t base = 64 * w; base < c; base += 64 * W) {
+            for (uint32_t base = QPW > 1 ? 0u : 64u * w; base < c; base += 64 * W) {
                 const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
                 const uint32_t myrow = sel ? sel_row
                                      : all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc])
@@ -401,7 +410,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
             }
             __syncthreads();  // part is the next item's LDS stage
         }
-        if (w == 0) {
+        if (QPW > 1 || w == 0) {
             L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
             bool certified = false;
             if (a.excl_out) {
@@ -489,7 +498,7 @@ __global__ __launch_bounds__(64 * W) void k_rescore(RescoreArgs a) {
         // them once it sees the flag.
         __shared__ uint32_t s_last;
         __syncthreads();  // (s_wrote final)
-        if (s_wrote || (!a.hres_idx && blockIdx.x < n_items)) __threadfence();
+        if (s_wrote || (!a.hres_idx && blockIdx.x * QPW < n_items)) __threadfence();
         if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();  // (wave 0 wrote them)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -924,12 +933,13 @@ hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     const uint32_t e = (a.k + 63) / 64;
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
     const bool dev = a.n_items_dev != nullptr;
-    const dim3 g(dev ? std::min<uint32_t>(a.n_items, kRescoreAllGrid) : a.n_items), b(dev ? 512 : 64);
+    // (one item per wave: four independent waves per workgroup, one workgroup per CU)
+    const dim3 g(dev ? std::min<uint32_t>(a.n_items, kRescoreAllGrid) : (a.n_items + 3) / 4), b(dev ? 512 : 256);
 #define BSR_RESCORE(E)                                                                        \
     do {                                                                                      \
         if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);                     \
-        else if (a.excl_out) hipLaunchKernelGGL((k_rescore<E, 1, BSR_GT_RESCORE_P>), g, b, 0, s, a); \
-        else hipLaunchKernelGGL((k_rescore<E, 1, 2>), g, b, 0, s, a);                         \
+        else if (a.excl_out) hipLaunchKernelGGL((k_rescore<E, 1, BSR_GT_RESCORE_P, 4>), g, b, 0, s, a); \
+        else hipLaunchKernelGGL((k_rescore<E, 1, 2, 4>), g, b, 0, s, a);                      \
     } while (0)
     switch (e) {
         case 1: BSR_RESCORE(1); break;
