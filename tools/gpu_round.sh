@@ -28,6 +28,7 @@
 #   looprec     record an 8-rank host-transport run's all-gathers ($O/loop8.npz) for the loopback steps below
 #   rstamps     phase stamps of the global-threshold rescore (lab-stamps build; after looprec)
 #   looptl      rocprofv3 kernel trace of the loopback step (replaying looprec) -> per-search timeline
+#   loopapi     rocprofv3 HIP API + kernel trace of the loopback step -> the host's calls between searches
 #   abloop:A,B  the loopback step with alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree)
 #   mpub        tools/microbench/merge_pub with and without the host-row writers' system-scope release
 #   mrfull      the full-size 8-rank global-threshold tests (configs[2], configs[4])
@@ -140,6 +141,10 @@ for step in $STEPS; do
     rstamps)
       BSR_LIB=tools/ab/libbsr_stamps.so run 300 "rescore stamps gtau" "$O/rstamps_gtau.txt" python tools/diag/rescore_stamps_gtau.py "$O/loop8.npz"
       grep -v amdgpu.ids "$O/rstamps_gtau.txt" ;;
+    loopapi)
+      run 300 "loopback api trace" "$O/bench_loop8_api.json" rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$O/apiloop" -o run -- \
+          python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 $NOB
+      python3 tools/diag/api_gap.py "$O/apiloop" > "$O/api_gap_loop8.txt"; cat "$O/api_gap_loop8.txt" ;;
     looptl)
       run 300 "loopback trace" "$O/bench_loop8_prof.json" rocprofv3 --kernel-trace --output-format csv -d "$O/tlloop" -o run -- \
           python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 $NOB
