@@ -476,9 +476,11 @@ def main():
             comm = bsr.Comm(uid[0], rank, world, device)
 
     lib = bsr.lib()
-    oi = np.empty((Q, K), np.uint64)
-    od = np.empty((Q, K), np.float32)
-    oc = np.empty(Q, np.uint32)
+    # the root's outputs in coherent pinned host memory: on the global-threshold path (N > 1) the
+    # merge writes the rows there directly, as a Rust caller using bsr_host_alloc would have it
+    oi = bsr.host_array((Q, K), np.uint64)
+    od = bsr.host_array((Q, K), np.float32)
+    oc = bsr.host_array(Q, np.uint32)
     comm_h = comm._h if comm else None
 
     def step(nq=Q, qptr=None, ix=index):

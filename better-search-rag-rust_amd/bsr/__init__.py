@@ -128,6 +128,8 @@ def lib() -> ctypes.CDLL:
         "bsr_gather_global_top_k": (ctypes.c_int, [_P, _P, _P, _P, u32, u32, _P, _P, _P]),
         "bsr_comm_init_loopback": (ctypes.c_int, [i32, i32, i32, u32, _P, _P, ctypes.POINTER(_P)]),
         "bsr_comm_loopback_stats": (ctypes.c_int, [_P, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "bsr_host_alloc": (ctypes.c_int, [u64, ctypes.POINTER(_P)]),
+        "bsr_host_free": (None, [_P]),
         "bsr_broadcast": (ctypes.c_int, [_P, _P, u64, i32]),
         "bsr_allgather_bytes": (ctypes.c_int, [_P, _P, _P, u64]),
         "bsr_parallel_top_k_similarity_search": (ctypes.c_int, [_P, _P, _P, u32, u32, _P, _P, _P]),
@@ -165,6 +167,30 @@ def _ptr(a) -> Optional[int]:
     if hasattr(a, "data_ptr"):
         return a.data_ptr()
     raise TypeError(f"unsupported buffer type {type(a)}")
+
+
+class _PinnedOwner:
+    def __init__(self, p):
+        self.p = p
+
+    def __del__(self):
+        try:
+            lib().bsr_host_free(self.p)
+        except Exception:
+            pass
+
+
+def host_array(shape, dtype) -> np.ndarray:
+    """A numpy array in coherent pinned host memory (bsr_host_alloc; freed with the array).  Root
+    outputs there are written by the GPU directly on the global-threshold path (include/bsr.h)."""
+    dtype = np.dtype(dtype)
+    shape = (shape,) if isinstance(shape, int) else tuple(shape)
+    n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    p = _P()
+    _check(lib().bsr_host_alloc(max(n, 1), ctypes.byref(p)))
+    buf = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+    buf._owner = _PinnedOwner(p.value)  # (the array's base keeps the allocation alive)
+    return np.frombuffer(buf, dtype=dtype, count=n // dtype.itemsize).reshape(shape)
 
 
 def device_count() -> int:

@@ -473,6 +473,18 @@ int bsr_comm_init_loopback(int32_t rank, int32_t size, int32_t device, uint32_t 
     BSR_GUARD(comm_init_loopback_impl(rank, size, device, n_calls, call_bytes, script, out));
 }
 
+int bsr_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return set_error(BSR_E_INVALID, "null argument");
+    *out = nullptr;
+    BSR_TRY(select_device(-1));
+    BSR_HIP(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocCoherent));
+    return BSR_OK;
+}
+
+void bsr_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int bsr_comm_loopback_stats(const bsr_comm* c, uint64_t* replayed, uint64_t* missed) {
     if (!c || !replayed || !missed) return set_error(BSR_E_INVALID, "null argument");
     if (!c->loopback) return set_error(BSR_E_INVALID, "not a loopback communicator");
@@ -911,10 +923,21 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     ma.pub_dst = c->h_mres_dev;
     // (the status words and F; the root's merged rows are written through by the merging waves)
     ma.pub_bytes = o_cnt;
+    // Root outputs in coherent pinned host memory (bsr_host_alloc): the merging waves write the
+    // merged rows straight into them -- no staging copy after the flag (round 5)
+    uint64_t* d_oi = nullptr;
+    float* d_od = nullptr;
+    uint32_t* d_oc = nullptr;
+    if (root && nq) {
+        d_oi = static_cast<uint64_t*>(coherent_host_alias(out_idx));
+        d_od = static_cast<float*>(coherent_host_alias(out_dist));
+        d_oc = static_cast<uint32_t*>(coherent_host_alias(out_count));
+    }
+    const bool direct = d_oi && d_od && d_oc;
     if (root) {
-        ma.hout_idx = reinterpret_cast<uint64_t*>(c->h_mres_dev + o_idx);
-        ma.hout_dist = reinterpret_cast<float*>(c->h_mres_dev + o_dist);
-        ma.hout_count = reinterpret_cast<uint32_t*>(c->h_mres_dev + o_cnt);
+        ma.hout_idx = direct ? d_oi : reinterpret_cast<uint64_t*>(c->h_mres_dev + o_idx);
+        ma.hout_dist = direct ? d_od : reinterpret_cast<float*>(c->h_mres_dev + o_dist);
+        ma.hout_count = direct ? d_oc : reinterpret_cast<uint32_t*>(c->h_mres_dev + o_cnt);
     }
     ma.pub_flag = c->h_flag_dev;
     ma.pub_ticket = c->pub_ticket.as<uint32_t>();
@@ -937,9 +960,9 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // 4. the uncertified queries, collectively (every rank holds the same F)
     const uint32_t nf = hw[0];
     ix->stats.n_fallback = nf;
-    uint32_t* m_cnt = reinterpret_cast<uint32_t*>(hm + o_cnt);
-    float* m_dist = reinterpret_cast<float*>(hm + o_dist);
-    uint64_t* m_idx = reinterpret_cast<uint64_t*>(hm + o_idx);
+    uint32_t* m_cnt = direct ? out_count : reinterpret_cast<uint32_t*>(hm + o_cnt);
+    float* m_dist = direct ? out_dist : reinterpret_cast<float*>(hm + o_dist);
+    uint64_t* m_idx = direct ? out_idx : reinterpret_cast<uint64_t*>(hm + o_idx);
     int fr = BSR_OK;  // the fallback's status (BSR_PARTIAL on a root whose own search failed)
     if (nf) {
         // (staging reserved by gtau_reserve: these resizes do not allocate.  A local failure
@@ -984,6 +1007,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
             }
     }
     if (!root) return clear_counts(out_count, nq);
+    if (direct) return fr;  // (the merged rows, and any fallback rows patched above, are in out_*)
     if (is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count)) {
         BSR_HIP_OR_HOST_COPY(out_idx, m_idx, nqk * sizeof(uint64_t));
         BSR_HIP_OR_HOST_COPY(out_dist, m_dist, nqk * sizeof(float));

@@ -105,6 +105,21 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+// The device address of coherent (fine-grained) pinned host memory -- hipHostMalloc with
+// hipHostMallocCoherent, e.g. bsr_host_alloc -- else nullptr (pageable memory, device memory,
+// or non-coherent pinned memory, which the host could read stale from its caches).
+void* coherent_host_alias(const void* p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (attr.type != hipMemoryTypeHost || !(attr.allocationFlags & hipHostMallocCoherent) || !attr.devicePointer)
+        return nullptr;
+    return attr.devicePointer;
+}
+
 int select_device(int device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {

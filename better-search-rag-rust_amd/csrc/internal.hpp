@@ -47,6 +47,7 @@ struct DevBuf {
 };
 
 bool is_device_ptr(const void* p);
+void* coherent_host_alias(const void* p);  // device address of coherent pinned host memory, or nullptr
 hipError_t stream_wait(hipStream_t s);  // poll until the stream's work is done
 // Poll a host flag a publishing kernel raises (checking the stream now and then): hipSuccess,
 // the stream's error, or hipErrorUnknown when the stream finished without raising it.

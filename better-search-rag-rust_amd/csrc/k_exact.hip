@@ -747,17 +747,38 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t off_l = incl - c_l;
         bool nan = false;
-        for (uint32_t l = 0; l < P; ++l) {
-            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, (int)l);
-            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)l);
-            const uint64_t bi = (uint64_t)l * a.idx_stride + (uint64_t)q * k_in;
-            const uint64_t bd = (uint64_t)l * a.dist_stride + (uint64_t)q * k_in;
-            for (uint32_t i = lane; i < c; i += kWave) {
-                const float d = dist[bd + i];
+        // The concatenation, position j = lane + 64 u: list l = the last with off_l <= j (P <= 64
+        // offsets, read lane by lane), then its entries -- every load of the query issued in one
+        // batch before any is consumed (round 5: a loop over the P lists issued them list by list,
+        // one memory latency per list, ~P latencies per merge)
+        constexpr int U = kMergeMaxEntries / kWave;
+        float dv[U];
+        uint64_t iv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = u * kWave + lane;
+            dv[u] = 0.0f;
+            iv[u] = 0;
+            if (u * kWave < (int)total && j < total) {
+                uint32_t l = 0, o = 0;
+                for (uint32_t m = 1; m < P; ++m) {
+                    const uint32_t om = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)m);
+                    if (om <= j) { l = m; o = om; }
+                }
+                const uint32_t i = j - o;
+                dv[u] = dist[(uint64_t)l * a.dist_stride + (uint64_t)q * k_in + i];
+                iv[u] = idx[(uint64_t)l * a.idx_stride + (uint64_t)q * k_in + i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = u * kWave + lane;
+            if (u * kWave < (int)total && j < total) {
+                const float d = dv[u];
                 nan |= d != d;
-                s_idx[o + i] = idx[bi + i];
-                s_dist[o + i] = d;
-                s_key[o + i] = ((uint64_t)ord_f32(d + 0.0f) << 32) | (o + i);  // (-0.0 + 0.0 = +0.0)
+                s_idx[j] = iv[u];
+                s_dist[j] = d;
+                s_key[j] = ((uint64_t)ord_f32(d + 0.0f) << 32) | j;  // (-0.0 + 0.0 = +0.0)
             }
         }
         __syncthreads();

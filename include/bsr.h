@@ -239,6 +239,13 @@ int bsr_parallel_top_k_similarity_search(bsr_comm* comm, bsr_index* ix, const fl
                                          uint32_t n_queries, uint32_t k, uint64_t* out_idx,
                                          float* out_dist, uint32_t* out_count);
 
+/* ---- pinned host buffers for results (round 5): coherent (fine-grained) pinned host memory.  Root
+ * outputs of bsr_parallel_top_k_similarity_search in such memory are written by the GPU directly
+ * on the global-threshold path (no staging copy after the search); any other host memory works
+ * everywhere, through a copy. -------------------------------------------------------------- */
+int bsr_host_alloc(uint64_t bytes, void** out);
+void bsr_host_free(void* p);
+
 /* ---- driver collectives: src/main.rs:123-125 (process_at_rank(ROOT).broadcast_into of the
  * query) and the timing gather of src/mpi_helpers/benchmark.rs:131-293.  Host or device
  * buffers; collective over the comm (RCCL or host transport). ------------------------ */

@@ -234,5 +234,18 @@ def test_loopback_replays_recorded_run(bsr_mod, gpu, corpus, tmp_path):
         _same({"idx": got[0], "dist": got[1], "cnt": got[2]},
               (res[0]["idx"], res[0]["dist"], res[0]["cnt"]))
     assert comm.loopback_stats() == (6, 0)
+    # root outputs in coherent pinned host memory: the merge writes the rows there directly
+    oi = bsr_mod.host_array((len(q), mr_worker.K), np.uint64)
+    od = bsr_mod.host_array((len(q), mr_worker.K), np.float32)
+    oc = bsr_mod.host_array(len(q), np.uint32)
+    oi[:] = 7
+    od[:] = -1.0
+    oc[:] = 999
+    qq = np.ascontiguousarray(q, np.float32)
+    st = bsr_mod.lib().bsr_parallel_top_k_similarity_search(comm._h, ix._h, qq.ctypes.data, len(q), mr_worker.K,
+                                                            oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+    assert st == 0, bsr_mod.lib().bsr_last_error()
+    _same({"idx": oi, "dist": od, "cnt": oc}, (res[0]["idx"], res[0]["dist"], res[0]["cnt"]))
+    assert comm.loopback_stats() == (9, 0)
     comm.close()
     ix.close()
