@@ -138,7 +138,10 @@ def lib() -> ctypes.CDLL:
         "bsr_index_set_profile": (ctypes.c_int, [_P, ctypes.c_int]),
         "bsr_synth_uniform": (ctypes.c_int, [_P, u64, u64, u32, u64]),
     }
+    optional = {"bsr_host_alloc", "bsr_host_free"}  # (absent in older builds used for A/B runs)
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -185,6 +188,8 @@ def host_array(shape, dtype) -> np.ndarray:
     outputs there are written by the GPU directly on the global-threshold path (include/bsr.h)."""
     dtype = np.dtype(dtype)
     shape = (shape,) if isinstance(shape, int) else tuple(shape)
+    if not hasattr(lib(), "bsr_host_alloc"):  # (an older build: pageable memory)
+        return np.empty(shape, dtype)
     n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
     p = _P()
     _check(lib().bsr_host_alloc(max(n, 1), ctypes.byref(p)))
