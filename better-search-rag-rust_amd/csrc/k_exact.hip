@@ -731,13 +731,34 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
+    float x_l = INFINITY;  // (certification) list `lane`'s exclusion bound for q
     auto merge_query = [&]() -> bool {
         if (a.st_all && q == 0)  // every list's status words, compact
             for (uint32_t i = lane; i < P * kStWords; i += kWave)
                 a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
         if (q >= nq) return false;
-        // list l's count on lane l, its offset in the concatenation (exclusive prefix sum)
+        // ONE batch of loads for the whole query (round 5: they were three dependent rounds --
+        // counts, then each list's entries, then the certification bounds): every slot of every
+        // list (l, i < k_in), list l's count and exclusion bound on lane l; the slots past a
+        // list's count are loaded and dropped.
+        constexpr int U = kMergeMaxEntries / kWave;
+        const uint32_t slots = P * k_in;  // (<= kMergeMaxEntries)
+        float dv[U];
+        uint64_t iv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t f = u * kWave + lane;
+            dv[u] = 0.0f;
+            iv[u] = 0;
+            if (u * kWave < (int)slots && f < slots) {
+                const uint32_t l = f / k_in, i = f - l * k_in;
+                dv[u] = dist[(uint64_t)l * a.dist_stride + (uint64_t)q * k_in + i];
+                iv[u] = idx[(uint64_t)l * a.idx_stride + (uint64_t)q * k_in + i];
+            }
+        }
         const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
+        x_l = (a.excl && lane < (int)P) ? a.excl[(uint64_t)lane * a.excl_stride + q] : INFINITY;
+        // list l's offset in the concatenation (exclusive prefix sum of the counts)
         uint32_t incl = c_l;
     #pragma unroll
         for (int off = 1; off < kWave; off <<= 1) {
@@ -747,33 +768,15 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t off_l = incl - c_l;
         bool nan = false;
-        // The concatenation, position j = lane + 64 u: list l = the last with off_l <= j (P <= 64
-        // offsets, read lane by lane), then its entries -- every load of the query issued in one
-        // batch before any is consumed (round 5: a loop over the P lists issued them list by list,
-        // one memory latency per list, ~P latencies per merge)
-        constexpr int U = kMergeMaxEntries / kWave;
-        float dv[U];
-        uint64_t iv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t j = u * kWave + lane;
-            dv[u] = 0.0f;
-            iv[u] = 0;
-            if (u * kWave < (int)total && j < total) {
-                uint32_t l = 0, o = 0;
-                for (uint32_t m = 1; m < P; ++m) {
-                    const uint32_t om = (uint32_t)__builtin_amdgcn_readlane((int)off_l, (int)m);
-                    if (om <= j) { l = m; o = om; }
-                }
-                const uint32_t i = j - o;
-                dv[u] = dist[(uint64_t)l * a.dist_stride + (uint64_t)q * k_in + i];
-                iv[u] = idx[(uint64_t)l * a.idx_stride + (uint64_t)q * k_in + i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = u * kWave + lane;
-            if (u * kWave < (int)total && j < total) {
+            const uint32_t f = u * kWave + lane;
+            const uint32_t l = f / (k_in ? k_in : 1u), i = f - l * k_in;
+            // (every lane takes part in the shuffles; l < P for the slots that exist)
+            const uint32_t cl = (uint32_t)__shfl((int)c_l, (int)(l < 64 ? l : 0), kWave);
+            const uint32_t ol = (uint32_t)__shfl((int)off_l, (int)(l < 64 ? l : 0), kWave);
+            if (u * kWave < (int)slots && f < slots && i < cl) {
+                const uint32_t j = ol + i;
                 const float d = dv[u];
                 nan |= d != d;
                 s_idx[j] = iv[u];
@@ -867,6 +870,10 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         }
         if (lane == 0) put_count(got);
         const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
+        // the smallest bound over the lists (NaN: nothing certifiable), loaded with the lists
+        float xmin = x_l == x_l ? x_l : -INFINITY;
+    #pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) xmin = fminf(xmin, __shfl_xor(xmin, off, kWave));
         bool shared = false;
         if (a.excl && lane == 0) {
             // Certification of a global-threshold parallel search: every row left
@@ -874,11 +881,6 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             // the merged list is the reference's iff it holds need = min(k, corpus rows) entries and
             // its k-th distance lies strictly below every rank's bound (a shorter list only when
             // every row of the corpus was a candidate: every bound +inf).
-            float xmin = INFINITY;
-            for (uint32_t l = 0; l < P; ++l) {
-                const float x = a.excl[(uint64_t)l * a.excl_stride + q];
-                xmin = x == x ? fminf(xmin, x) : -INFINITY;
-            }
             bool ok = got >= a.need;
             if (ok && got == k) {
                 ok = (double)s_dist[(uint32_t)kth] < (double)xmin;
