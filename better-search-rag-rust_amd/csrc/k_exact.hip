@@ -4,6 +4,7 @@
 // Compiled with -ffp-contract=off: every f32 multiply and add rounds separately, in index
 // order, exactly as src/metrics.rs:153-155 does; sqrt is __builtin_sqrtf (correctly
 // rounded) and `/` is the correctly rounded division (see bsr_device.hpp).
+#include <cstdlib>
 #include "bsr_device.hpp"
 #include "kernels.hpp"
 
@@ -135,6 +136,95 @@ __device__ __forceinline__ void seq_chunk(const float* __restrict__ my, const fl
 // load in flight -- vmcnt(0) -- and serialise the two-chunk prefetch below.)
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
+// Mode S's candidate selection, one wave: the (kp+1)-th smallest of the c emitted keys xk (cap <=
+// 1024: 16 registers, kp <= 63) by radix select -- the high words first (score bits: only the bits
+// below the highest one in which the emitted keys differ are searched), then, only when several
+// keys share the K-th high word, the low words (rows) among those -- and the kp keys below it
+// compacted through lsel (LDS, 64 words): lane l's row in sel_row (l < c on return).  tx_sel: the
+// (kp+1)-th score (every row left out is at most that), or tau0 when every emitted row is a
+// candidate; INFINITY for an overflowed list.
+__device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c, bool overflow, uint32_t kp,
+                                          float tau0, float& tx_sel, uint32_t* lsel, uint32_t& sel_row, int lane) {
+    constexpr int NR = 16;
+    uint64_t x[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const uint32_t i = j * kWave + lane;
+        x[j] = i < c ? xk[j] : kKeyNone;
+    }
+    uint64_t T = kKeyNone;
+    if (!overflow && c > kp) {
+        const uint32_t K = kp + 1;
+        uint32_t hmin = ~0u, hmax = 0;
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+            if (x[j] != kKeyNone) {
+                hmin = min(hmin, (uint32_t)(x[j] >> 32));
+                hmax = max(hmax, (uint32_t)(x[j] >> 32));
+            }
+        hmin = wave_reduce_u32(hmin, [](uint32_t a, uint32_t b) { return min(a, b); });
+        hmax = wave_reduce_u32(hmax, [](uint32_t a, uint32_t b) { return max(a, b); });
+        const uint32_t diff = hmin ^ hmax;
+        const int top = diff ? 31 - __builtin_clz(diff) : -1;
+        // (top < 0: every key has the same high word)
+        uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
+        for (int b = top; b >= 0; --b) {
+            const uint32_t t = Th | (1u << b);
+            uint32_t below = 0;
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+                if (j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
+            if (below < K) Th = t;
+        }
+        uint32_t lt = 0, eq = 0;
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+            if (j * kWave < (int)c) {
+                const uint32_t h = (uint32_t)(x[j] >> 32);
+                lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
+                eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
+            }
+        const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
+        uint32_t Tl = 0;
+        if (eq > 1)
+            for (int b = 31; b >= 0; --b) {
+                const uint32_t t = Tl | (1u << b);
+                uint32_t below = 0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j)
+                    if (j * kWave < (int)c)
+                        below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
+                if (below < K2) Tl = t;
+            }
+        else
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {  // the one key with high word Th
+                const uint64_t m = __ballot(x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th);
+                if (m) Tl = (uint32_t)__shfl((int)(uint32_t)x[j], __builtin_ctzll(m), kWave);
+            }
+        T = ((uint64_t)Th << 32) | Tl;
+        tx_sel = score_key_score(T);
+        c = kp;
+    } else if (!overflow) {
+        tx_sel = tau0;  // every emitted row is a candidate; tau0 bounds the rest
+    }
+    uint32_t base = 0;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const bool pick = x[j] < T;
+        const uint64_t m = __ballot(pick);
+        if (pick) {
+            const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            lsel[pos] = key_row(x[j]);
+        }
+        base += (uint32_t)__popcll(m);
+    }
+    wave_sync();
+    sel_row = lane < (int)c ? lsel[lane] : 0u;
+    wave_sync();
+}
+
 // W waves per workgroup, one query per workgroup at a time: wave w takes candidates
 // w*64 + lane, + 64W, ...; the W per-wave lists merge through LDS.  W = 1: one wave per
 // query (the k' selected candidates, every query).  W = 8: the queries that failed
@@ -237,91 +327,8 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
         uint32_t c = overflow ? 0u : cnt;
         float tx_sel = INFINITY;
         uint32_t sel_row = 0;
-        if (W == 1 && sel) {
-            // the (kp+1)-th smallest key T by radix select over the emitted keys (cap <= 1024:
-            // 16 registers), the kp keys below it compacted through LDS; kp <= 63 (one pass)
-            uint64_t x[NR];
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const uint32_t i = j * kWave + lane;
-                x[j] = i < c ? xk[j] : kKeyNone;
-            }
-            uint64_t T = kKeyNone;
-            if (!overflow && c > a.kp) {
-                // the high words first (score bits: only the bits below the highest one in which
-                // the emitted keys differ are searched), then -- only when several keys share
-                // the K-th high word -- the low words (rows) among those
-                const uint32_t K = a.kp + 1;
-                uint32_t hmin = ~0u, hmax = 0;
-#pragma unroll
-                for (int j = 0; j < NR; ++j)
-                    if (x[j] != kKeyNone) {
-                        hmin = min(hmin, (uint32_t)(x[j] >> 32));
-                        hmax = max(hmax, (uint32_t)(x[j] >> 32));
-                    }
-                hmin = wave_reduce_u32(hmin, [](uint32_t a, uint32_t b) { return min(a, b); });
-                hmax = wave_reduce_u32(hmax, [](uint32_t a, uint32_t b) { return max(a, b); });
-                const uint32_t diff = hmin ^ hmax;
-                const int top = diff ? 31 - __builtin_clz(diff) : -1;
-                // (top < 0: every key has the same high word)
-                uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
-                for (int b = top; b >= 0; --b) {
-                    const uint32_t t = Th | (1u << b);
-                    uint32_t below = 0;
-#pragma unroll
-                    for (int j = 0; j < NR; ++j)
-                        if (j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
-                    if (below < K) Th = t;
-                }
-                uint32_t lt = 0, eq = 0;
-#pragma unroll
-                for (int j = 0; j < NR; ++j)
-                    if (j * kWave < (int)c) {
-                        const uint32_t h = (uint32_t)(x[j] >> 32);
-                        lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
-                        eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
-                    }
-                const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
-                uint32_t Tl = 0;
-                if (eq > 1)
-                    for (int b = 31; b >= 0; --b) {
-                        const uint32_t t = Tl | (1u << b);
-                        uint32_t below = 0;
-#pragma unroll
-                        for (int j = 0; j < NR; ++j)
-                            if (j * kWave < (int)c)
-                                below += (uint32_t)__popcll(
-                                    __ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
-                        if (below < K2) Tl = t;
-                    }
-                else
-#pragma unroll
-                    for (int j = 0; j < NR; ++j) {  // the one key with high word Th
-                        const uint64_t m = __ballot(x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th);
-                        if (m) Tl = (uint32_t)__shfl((int)(uint32_t)x[j], __builtin_ctzll(m), kWave);
-                    }
-                T = ((uint64_t)Th << 32) | Tl;
-                tx_sel = score_key_score(T);
-                c = a.kp;
-            } else if (!overflow) {
-                tx_sel = a.tau0[q];  // every emitted row is a candidate; tau0 bounds the rest
-            }
-            uint32_t* const lsel = reinterpret_cast<uint32_t*>(lds);
-            uint32_t base = 0;
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const bool pick = x[j] < T;
-                const uint64_t m = __ballot(pick);
-                if (pick) {
-                    const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    lsel[pos] = key_row(x[j]);
-                }
-                base += (uint32_t)__popcll(m);
-            }
-            wave_sync();
-            sel_row = lane < (int)c ? lsel[lane] : 0u;
-            wave_sync();
+        if constexpr (W == 1) {
+            if (sel) select_kp(xk, c, overflow, a.kp, a.tau0[q], tx_sel, reinterpret_cast<uint32_t*>(lds), sel_row, lane);
         }
         BSR_STAMP(W, 2);
         const float mag_b = a.nb[q];
@@ -514,6 +521,149 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
             }
         }
     }
+}
+
+
+// ------------------------------------------------------------------------------------
+// The first rescore pass of a tiny batch (<= 16 queries: the single-query p50 path), mode S
+// (round 5): ONE workgroup per query with one wave per 64-float chunk of the rows (ld / 64 <= 16
+// waves).  Wave 0 selects the k' candidates (select_kp); then every wave loads ITS chunk of every
+// candidate row at once, coalesced -- all of a row's loads in flight together, one memory latency
+// instead of one per chunk -- and the reference's sequential sum runs through the waves in chunk
+// order, each transposing its chunk through an LDS stage and continuing the running dot /
+// max|a-b| it reads from LDS (a workgroup barrier per chunk).  (A first version loaded each
+// lane's own row, 64 cache lines per instruction: the one CU's address path made it slower than
+// the one-wave kernel.)  The
+// arithmetic and its order are k_rescore's, so the distances are its bits; wave 0 finishes
+// (top-k, certification, result rows) as k_rescore mode S does.  One-wave k_rescore spent ~30 us
+// on one query's 63 rows: 12 chunks, each behind its own load latency.
+// ------------------------------------------------------------------------------------
+constexpr int kKpStage = 64 * 68;  // 64 rows x one chunk (stride 68)
+template <int E>
+__global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ __attribute__((aligned(16))) float ldq[1024];
+    __shared__ __attribute__((aligned(16))) float stage[2 * kKpStage];
+    __shared__ float s_acc[64], s_mx[64];
+    __shared__ uint32_t lsel[64];
+    __shared__ uint32_t s_c, s_ov;
+    __shared__ float s_tx;
+    const uint32_t item = blockIdx.x;
+    if (item >= a.n_items) return;  // (grid = n_items: uniform per workgroup)
+    const uint32_t q = a.qlist ? a.qlist[item] : item;
+    const uint32_t ld = a.ld, dim = a.dim;
+    // the query's chunk of this wave, staged in LDS (read as broadcasts)
+    if ((uint32_t)(w * 64 + lane) < ld) ldq[w * 64 + lane] = a.qf32[(uint64_t)q * ld + w * 64 + lane];
+    if (w == 0) {
+        constexpr int NR = 16;
+        uint64_t xk[NR];
+        const uint64_t* src = a.cand_keys + (uint64_t)q * a.cap;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const uint32_t i = j * kWave + lane;
+            xk[j] = i < a.cap ? src[i] : kKeyNone;
+        }
+        const uint32_t cnt = a.cnt[q];
+        const bool overflow = cnt > a.cap;
+        uint32_t c = overflow ? 0u : cnt;
+        float tx = INFINITY;
+        uint32_t sel_row = 0;
+        select_kp(xk, c, overflow, a.kp, a.tau0[q], tx, lsel, sel_row, lane);
+        if (lane == 0) {
+            s_c = c;
+            s_tx = tx;
+            s_ov = overflow ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t c = s_c;
+    const uint32_t myrow = lane < (int)c ? lsel[lane] : (c ? lsel[0] : 0u);
+    // this wave's chunk of the 64 rows, coalesced (a quarter wave per row, 16 loads in flight)
+    uint32_t lrow[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
+    f32x4_t pre[16];
+    load_cand_chunk(pre, a.rows, ld, lrow, (uint32_t)w, lane);
+    // Two LDS stages: while wave s walks its rows from stage s & 1, wave s + 1 transposes its
+    // chunk into the other (last read by wave s - 1, before the previous barrier)
+    auto put = [&](float* st) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int L16 = i * 64 + lane;
+            *reinterpret_cast<f32x4_t*>(st + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
+        }
+    };
+    if (w == 0) put(stage);
+    __syncthreads();
+    for (int step = 0; step < nw; ++step) {
+        if (w == step) {
+            float acc[1] = {step ? s_acc[lane] : -0.0f}, mx[1] = {step ? s_mx[lane] : 0.0f};
+            const float* const bb[1] = {ldq + w * 64};
+            const uint32_t nvalid = dim > (uint32_t)w * 64 ? min(64u, dim - (uint32_t)w * 64) : 0u;
+            seq_chunk<1>(stage + (step & 1) * kKpStage + lane * 68, bb, nvalid, acc, mx);
+            s_acc[lane] = acc[0];
+            s_mx[lane] = mx[0];
+        } else if (w == step + 1) {
+            put(stage + (w & 1) * kKpStage);
+        }
+        __syncthreads();
+    }
+    if (w != 0) return;
+    const float mag_b = a.nb[q];
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    {
+        const float d = finish_distance(s_acc[lane], s_mx[lane], a.na[myrow], mag_b);
+        L.offer(lane < (int)c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
+    }
+    L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
+    bool certified = false;
+    if (lane == 0) {
+        // certification, as k_rescore mode S
+        const float tx = s_ov ? INFINITY : s_tx;
+        const double ebound = (double)a.ebound[q];
+        bool ok;
+        if (tx == -INFINITY) {
+            ok = true;
+        } else if (!(tx < INFINITY) || thr == kKeyNone) {
+            ok = false;
+        } else {
+            const double dk = (double)key_dist(thr);
+            ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
+                 (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
+        }
+        if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
+        certified = ok;
+    }
+    bool host_rows = false;
+    if (a.res_idx && __shfl((int)certified, 0, kWave)) {
+        const uint32_t cnt = (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = e * kWave + lane;
+            if (i < a.k) {
+                const uint64_t key = L.v[e];
+                const bool has = i < cnt && key != kKeyNone;
+                const uint64_t gi = has ? a.offset + key_row(key) : ~0ull;
+                const float gd = has ? key_dist(key) : INFINITY;
+                a.res_idx[(uint64_t)q * a.k + i] = gi;
+                a.res_dist[(uint64_t)q * a.k + i] = gd;
+                if (a.hres_idx) {
+                    host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
+                    host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
+                    host_rows = true;
+                }
+            }
+        }
+        if (lane == 0) {
+            a.res_cnt[q] = cnt;
+            if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
+        }
+        host_rows = host_rows || a.hres_cnt != nullptr;
+    }
+    // (the first pass: the host reads these rows once the batch's last kernel raises its flag)
+    if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();
 }
 
 // ------------------------------------------------------------------------------------
@@ -954,6 +1104,17 @@ extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     if (!a.n_items) return hipSuccess;
     const uint32_t e = (a.k + 63) / 64;
+    // the first pass (mode S) of a tiny batch: one workgroup per query, one wave per chunk
+    // (BSR_RESCORE_KP=0: the one-wave kernel instead, for A/B runs)
+    static const bool kp_on = [] {
+        const char* v = getenv("BSR_RESCORE_KP");
+        return !(v && v[0] == '0');
+    }();
+    if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && a.n_items <= 16 && a.ld % 64 == 0 &&
+        a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && a.cap <= 1024) {
+        hipLaunchKernelGGL(k_rescore_kp<1>, dim3(a.n_items), dim3(a.ld), 0, s, a);
+        return hipGetLastError();
+    }
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
     const bool dev = a.n_items_dev != nullptr;
     // (one item per wave: four independent waves per workgroup, one workgroup per CU)

@@ -65,6 +65,27 @@ for step in $STEPS; do
       run 300 "bench c2" "$O/bench_c2.json" python bench.py --config c2 --steps 20 --warmup 3 --verify 2 $NOB
       run 300 "bench c4" "$O/bench_c4.json" python bench.py --config c4 --steps 5 --warmup 2 --verify 2 $NOB
       run 300 "bench c5" "$O/bench_c5.json" python bench.py --config c5 --steps 5 --warmup 2 --verify 2 $NOB ;;
+    p50ab)
+      # the tiny-batch rescore (k_rescore_kp) against the one-wave kernel, same process build,
+      # interleaved: p50 of one query over the default corpus and its kernels
+      for r in 1 2; do
+        for v in 1 0; do
+          BSR_RESCORE_KP=$v run 200 "p50 kp=$v $r" "$O/p50ab_${v}_$r.json" python bench.py --steps 3 --warmup 2 \
+              --verify 0 --p50-iters 200 $NOB
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('kp', sys.argv[2], d['p50_ms'], d.get('p50_kernels_ms_rank0'))" \
+              "$O/p50ab_${v}_$r.json" "$v"
+        done
+      done ;;
+    p50rs)
+      # the single-query rescore kernels, kp on / off, two rounds (tools/diag/p50_rescore.py)
+      for r in 1 2; do
+        for v in 1 0; do
+          for nq in 1 16; do
+            BSR_RESCORE_KP=$v timeout -k 10 200 python3 tools/diag/p50_rescore.py 2000000 $nq >> "$O/p50rs.txt" 2>> "$O/err.txt" || exit 1
+          done
+        done
+      done
+      cat "$O/p50rs.txt" ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
