@@ -503,16 +503,19 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
         // a host mirror, the result rows it wrote.  A workgroup that wrote result rows into the host
         // mirror releases them at system scope (BSR_PUB_SYSREL) before its ticket: the host reads
         // them once it sees the flag.
+        // (a one-workgroup grid -- a tiny batch's second chance -- is its own last arrival: no
+        // agent fences, no ticket)
+        const bool solo = gridDim.x == 1;
         __shared__ uint32_t s_last;
         __syncthreads();  // (s_wrote final)
-        if (s_wrote || (!a.hres_idx && blockIdx.x * QPW < n_items)) __threadfence();
+        if (!solo && (s_wrote || (!a.hres_idx && blockIdx.x * QPW < n_items))) __threadfence();
         if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();  // (wave 0 wrote them)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
+        if (threadIdx.x == 0) s_last = solo || last_arrival(a.pub_ticket) ? 1u : 0u;
         __syncthreads();
         if (s_last) {
-            __threadfence();
+            if (!solo) __threadfence();
             publish_copy(a.pub_src, a.pub_dst, a.pub_bytes, threadIdx.x, blockDim.x);
             __threadfence_system();
             __syncthreads();
@@ -544,12 +547,13 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     __shared__ __attribute__((aligned(16))) float ldq[1024];
     __shared__ __attribute__((aligned(16))) float stage[2 * kKpStage];
-    __shared__ float s_acc[64], s_mx[64];
+    __shared__ float s_acc[64], s_mxw[16][64];
     __shared__ uint32_t lsel[64];
     __shared__ uint32_t s_c, s_ov;
     __shared__ float s_tx;
     const uint32_t item = blockIdx.x;
     if (item >= a.n_items) return;  // (grid = n_items: uniform per workgroup)
+    if (w == 0) BSR_STAMP(1, 0);
     const uint32_t q = a.qlist ? a.qlist[item] : item;
     const uint32_t ld = a.ld, dim = a.dim;
     // the query's chunk of this wave, staged in LDS (read as broadcasts)
@@ -574,6 +578,7 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
             s_tx = tx;
             s_ov = overflow ? 1u : 0u;
         }
+        BSR_STAMP(1, 1);
     }
     __syncthreads();
     const uint32_t c = s_c;
@@ -584,8 +589,36 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
     f32x4_t pre[16];
     load_cand_chunk(pre, a.rows, ld, lrow, (uint32_t)w, lane);
-    // Two LDS stages: while wave s walks its rows from stage s & 1, wave s + 1 transposes its
-    // chunk into the other (last read by wave s - 1, before the previous barrier)
+    // The products x_i * b_i (rounded, as the reference's separate multiply rounds them) and
+    // max |x_i - b_i| (order-free, no NaN reaches here) need no order: every wave forms them for
+    // its chunk in place, at once.  Only the running sum is sequential.
+    const uint32_t nvalid = dim > (uint32_t)w * 64 ? min(64u, dim - (uint32_t)w * 64) : 0u;
+    {
+        const uint32_t c0 = (lane & 15) * 4;
+        const f32x4_t bq = *reinterpret_cast<const f32x4_t*>(ldq + w * 64 + c0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            f32x4_t x = pre[i];
+            float m = 0.0f;
+            if (c0 + 0 < nvalid) m = fmaxf(m, fabsf(x.x - bq.x));
+            if (c0 + 1 < nvalid) m = fmaxf(m, fabsf(x.y - bq.y));
+            if (c0 + 2 < nvalid) m = fmaxf(m, fabsf(x.z - bq.z));
+            if (c0 + 3 < nvalid) m = fmaxf(m, fabsf(x.w - bq.w));
+            x.x = x.x * bq.x;
+            x.y = x.y * bq.y;
+            x.z = x.z * bq.z;
+            x.w = x.w * bq.w;
+            pre[i] = x;
+            // the row's maximum over this chunk: its 16 lanes
+            m = fmaxf(m, __shfl_xor(m, 1, kWave));
+            m = fmaxf(m, __shfl_xor(m, 2, kWave));
+            m = fmaxf(m, __shfl_xor(m, 4, kWave));
+            m = fmaxf(m, __shfl_xor(m, 8, kWave));
+            if ((lane & 15) == 0) s_mxw[w][4 * i + (lane >> 4)] = m;
+        }
+    }
+    // Two LDS stages of products: while wave s sums its rows' from stage s & 1, wave s + 1
+    // transposes its chunk into the other (last read by wave s - 1, before the previous barrier)
     auto put = [&](float* st) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -595,26 +628,40 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     };
     if (w == 0) put(stage);
     __syncthreads();
+    if (w == 0) BSR_STAMP(1, 2);
+    float acc = -0.0f;
     for (int step = 0; step < nw; ++step) {
         if (w == step) {
-            float acc[1] = {step ? s_acc[lane] : -0.0f}, mx[1] = {step ? s_mx[lane] : 0.0f};
-            const float* const bb[1] = {ldq + w * 64};
-            const uint32_t nvalid = dim > (uint32_t)w * 64 ? min(64u, dim - (uint32_t)w * 64) : 0u;
-            seq_chunk<1>(stage + (step & 1) * kKpStage + lane * 68, bb, nvalid, acc, mx);
-            s_acc[lane] = acc[0];
-            s_mx[lane] = mx[0];
+            if (step) acc = s_acc[lane];
+            const float* my = stage + (step & 1) * kKpStage + lane * 68;
+            if (nvalid == 64) {
+#pragma unroll
+                for (int i = 0; i < 64; i += 4) {
+                    const f32x4_t x = *reinterpret_cast<const f32x4_t*>(my + i);
+                    acc = acc + x.x;
+                    acc = acc + x.y;
+                    acc = acc + x.z;
+                    acc = acc + x.w;
+                }
+            } else {
+                for (uint32_t i = 0; i < nvalid; ++i) acc = acc + my[i];
+            }
+            s_acc[lane] = acc;
         } else if (w == step + 1) {
             put(stage + (w & 1) * kKpStage);
         }
         __syncthreads();
     }
     if (w != 0) return;
+    BSR_STAMP(1, 3);
     const float mag_b = a.nb[q];
     WaveTopK<E> L;
     L.init();
     uint64_t thr = kKeyNone;
     {
-        const float d = finish_distance(s_acc[lane], s_mx[lane], a.na[myrow], mag_b);
+        float mx = 0.0f;
+        for (int v = 0; v < nw; ++v) mx = fmaxf(mx, s_mxw[v][lane]);
+        const float d = finish_distance(s_acc[lane], mx, a.na[myrow], mag_b);  // (the last wave's sum)
         L.offer(lane < (int)c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
     }
     L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
@@ -664,6 +711,7 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     }
     // (the first pass: the host reads these rows once the batch's last kernel raises its flag)
     if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();
+    BSR_STAMP(1, 4);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1098,6 +1146,9 @@ extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
 #endif
 // Chunks of candidate rows in flight in the global-threshold search's rescore of every emitted
 // row (one wave per query, ~32 rows per query per rank at N = 8: latency-bound, not HBM-bound).
+#ifndef BSR_GT_RESCORE_W  // (lab) 2: the global threshold's rescore with two waves per query
+#define BSR_GT_RESCORE_W 1
+#endif
 #ifndef BSR_GT_RESCORE_P
 #define BSR_GT_RESCORE_P 2
 #endif
@@ -1118,10 +1169,14 @@ hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
     const bool dev = a.n_items_dev != nullptr;
     // (one item per wave: four independent waves per workgroup, one workgroup per CU)
-    const dim3 g(dev ? std::min<uint32_t>(a.n_items, kRescoreAllGrid) : (a.n_items + 3) / 4), b(dev ? 512 : 256);
+    // (a tiny batch's second chance: one workgroup, its own last arrival -- rarely any item)
+    const uint32_t gdev = a.n_items <= 16 ? 1u : std::min<uint32_t>(a.n_items, kRescoreAllGrid);
+    const dim3 g(dev ? gdev : (a.n_items + 3) / 4), b(dev ? 512 : 256);
 #define BSR_RESCORE(E)                                                                        \
     do {                                                                                      \
         if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);                     \
+        else if (a.excl_out && BSR_GT_RESCORE_W == 2)                                        \
+            hipLaunchKernelGGL((k_rescore<E, 2, BSR_GT_RESCORE_P, 1>), dim3(a.n_items), dim3(128), 0, s, a); \
         else if (a.excl_out) hipLaunchKernelGGL((k_rescore<E, 1, BSR_GT_RESCORE_P, 4>), g, b, 0, s, a); \
         else hipLaunchKernelGGL((k_rescore<E, 1, 2, 4>), g, b, 0, s, a);                      \
     } while (0)

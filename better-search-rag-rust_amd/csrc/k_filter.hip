@@ -1315,6 +1315,9 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
 // SAMPLE: a wave takes the two units of one 32-sampled-row block back to back, so the
 // compact maximum over 32 sampled rows stays in a register.
 // ------------------------------------------------------------------------------------
+#ifndef BSR_SKINNY_NT
+#define BSR_SKINNY_NT 0
+#endif
 template <bool EMIT, int NK>
 __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1339,7 +1342,12 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
         const uint8_t* a = p.A + (uint64_t)r * p.a_stride + h * 16;
 #pragma unroll
         for (int s = 0; s < NK; ++s)
-            if (s < (int)nk) fa[s] = *reinterpret_cast<const i32x4_t*>(a + s * kSliceB);
+            if (s < (int)nk) {
+                if constexpr (EMIT && BSR_SKINNY_NT)  // (lab: the streamed rows marked non-temporal)
+                    fa[s] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(a + s * kSliceB));
+                else
+                    fa[s] = *reinterpret_cast<const i32x4_t*>(a + s * kSliceB);
+            }
     };
     float smax = -INFINITY;  // SAMPLE compact: running maximum of the 32-row block
     auto process = [&](const i32x4_t (&fa)[NK], uint32_t u) {
@@ -1552,6 +1560,77 @@ __global__ __launch_bounds__(256) void k_select_tau_w(const float* __restrict__ 
     if (smax) L.store(smax + (uint64_t)q * ks, (int)ks);
 }
 
+// The same selection for tiny batches (<= 16 queries: the single-query p50 path) over long sample
+// rows (n_s <= 16 x 64 NV): SIXTEEN waves per query, each holding a sixteenth of the row in
+// registers.  The lower bound lb is the largest of the waves' ks-th lane maxima (each a lower bound
+// of the query's ks-th value, as above); each wave keeps its own ks best among the values >= lb
+// (usually a few), and wave 0 merges the non-empty lists.  Exact, so tau and the ks best keys are
+// k_select_tau's, bit for bit; one 4-wave workgroup per query spent ~20 us at 10M rows.
+template <int NV>
+__global__ __launch_bounds__(1024) void k_select_tau_m(const float* __restrict__ S, uint32_t s_ld, uint32_t n_s,
+                                                       uint32_t nq, uint32_t qpad, const uint32_t* __restrict__ qflags,
+                                                       uint32_t ks, float* __restrict__ tau, uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ status, uint64_t* __restrict__ smax) {
+    constexpr int NW = 16;
+    const uint32_t q = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (q == 0 && t == 0) { status[kStFail] = 0; status[kStEmitted] = 0; status[kStFail2] = 0; }
+    if (q == 0)  // the emit filter's tail counters
+        for (uint32_t i = t; i < 8 * kTailCounters + kGangWords; i += blockDim.x) cnt[qpad + i] = 0;
+    if (q >= qpad) return;
+    if (t == 0) cnt[q] = 0;
+    const bool none = q >= nq || (qflags[q] & kQueryNoApprox);
+    if (smax && (none || n_s < ks))
+        for (uint32_t i = t; i < ks; i += blockDim.x) smax[(uint64_t)q * ks + i] = kKeyNone;
+    if (none) {
+        if (t == 0) tau[q] = INFINITY;  // never emits: answered by the exact scan
+        return;
+    }
+    if (n_s < ks) {
+        if (t == 0) tau[q] = -INFINITY;
+        return;
+    }
+    __shared__ float lbw[NW];
+    __shared__ uint64_t part[NW][kWave];
+    __shared__ uint32_t s_has;
+    if (t == 0) s_has = 0;
+    const float* s = S + (uint64_t)q * s_ld;
+    const uint32_t per = (n_s + NW - 1) / NW, lo = w * per, hi = lo + per < n_s ? lo + per : n_s;
+    float v[NV];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint32_t i = lo + j * kWave + lane;
+        v[j] = i < hi ? s[i] : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) m = fmaxf(m, v[j]);
+    const uint64_t sorted = wave_sort64(score_key(m, (uint32_t)lane));
+    if (lane == 0) lbw[w] = score_key_score(shfl64(sorted, (int)ks - 1));
+    __syncthreads();
+    float lb = lbw[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) lb = fmaxf(lb, lbw[i]);
+    WaveTopK<1> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint32_t i = lo + j * kWave + lane;
+        if (lo + j * kWave < hi) L.offer((i < hi && v[j] >= lb) ? score_key(v[j], i) : kKeyNone, (int)ks, thr);
+    }
+    part[w][lane] = L.v[0];
+    if (lane == 0 && L.v[0] != kKeyNone) atomicOr(&s_has, 1u << w);
+    __syncthreads();
+    if (w != 0) return;
+    WaveTopK<1> M;
+    M.init();
+    uint64_t mt = kKeyNone;
+    for (uint32_t h = s_has; h; h &= h - 1) M.offer(part[__builtin_ctz(h)][lane], (int)ks, mt);
+    if (lane == 0) tau[q] = score_key_score(mt);
+    if (smax) M.store(smax + (uint64_t)q * ks, (int)ks);
+}
+
 // The global emission threshold of a parallel search: tau[q] = the ks-th best
 // of the P ranks' ks best sample keys, all-gathered as g[P][qpad][ks] -- the threshold one
 // shard holding every rank's rows would select.  One wave per query, four per workgroup.
@@ -1722,7 +1801,10 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
                              hipStream_t s, uint64_t* smax) {
     if (ks > 2 * kWave) return hipErrorInvalidValue;
-    if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)
+    if (ks <= kWave && qpad <= 16 && n_s > 16 * kWave && n_s <= 16 * 16 * kWave)
+        hipLaunchKernelGGL(k_select_tau_m<16>, dim3(qpad), dim3(1024), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
+                           tau, cnt, status, smax);
+    else if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)
         hipLaunchKernelGGL(k_select_tau_w<32>, dim3(qpad / 4), dim3(256), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
                            tau, cnt, status, smax);
     else if (ks > kWave)

@@ -53,3 +53,16 @@ print(f"kp={os.environ.get('BSR_RESCORE_KP', '1')} rows {N} queries {Q}: wall me
       f"| level-2 span {p.search_ms / max(p.searches, 1) * 1e3:.1f} us, rescore {p.rescore_ms / max(p.rescore_launches, 1) * 1e3:.1f} us "
       f"x {p.rescore_launches / max(p.searches, 1):.2f}/search, emit {p.gemm_emit_ms / max(p.gemm_emit_launches, 1) * 1e3:.1f} us",
       flush=True)
+if os.environ.get("BSR_READ_STAMPS") == "1":
+    # the lab build's per-query phase stamps of the last search (make lab-stamps; kp kernel:
+    # 0 start, 1 keys + select, 2 rows of chunk 0 in LDS, 3 the 12 chunks walked, 4 finish)
+    import ctypes
+    st = np.zeros((4096, 8), np.uint64)
+    L.bsr_lab_rescore_stamps.restype = ctypes.c_int
+    assert L.bsr_lab_rescore_stamps(st.ctypes.data_as(ctypes.c_void_p), 4096) == 0
+    s = st[:Q, :5].astype(np.int64)
+    us = (s - s[:, :1]) / 100.0
+    for nm, i in (("keys + select", 1), ("rows -> LDS", 2), ("walk chunks", 3), ("finish", 4)):
+        d = us[:, i] - us[:, i - 1]
+        print(f"  {nm:16s} median {np.median(d):7.2f} max {d.max():7.2f} us", flush=True)
+    print(f"  {'total':16s} median {np.median(us[:, 4]):7.2f} max {us[:, 4].max():7.2f} us", flush=True)

@@ -86,6 +86,26 @@ for step in $STEPS; do
         done
       done
       cat "$O/p50rs.txt" ;;
+    p50st)
+      # the single query's rescore phases (lab stamps) and its kernel timeline (rocprof trace)
+      BSR_LIB=tools/ab/libbsr_stamps.so BSR_READ_STAMPS=1 timeout -k 10 200 python3 tools/diag/p50_rescore.py 2000000 1 \
+          > "$O/p50_stamps.txt" 2>> "$O/err.txt" || exit 1
+      cat "$O/p50_stamps.txt"
+      run 300 "p50 trace" "$O/p50_trace.txt" rocprofv3 --kernel-trace --output-format csv -d "$O/tlp50" -o run -- \
+          python3 tools/diag/p50_rescore.py 2000000 1
+      f=$(find "$O/tlp50" -name "*kernel_trace.csv" | head -1)
+      python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_p50.txt"; tail -30 "$O/timeline_p50.txt" ;;
+    p50lib:*)
+      # p50 of one query over the default corpus, per library (new = the tree's), interleaved
+      for r in 1 2; do
+        for v in $(echo "${step#*:}" | tr , ' '); do
+          if [ "$v" = new ]; then L=""; else L="tools/ab/libbsr_$v.so"; fi
+          BSR_LIB=$L run 200 "p50 $v $r" "$O/p50lib_${v}_$r.json" python bench.py --steps 3 --warmup 2 \
+              --verify 0 --p50-iters 200 $NOB
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('p50', sys.argv[2], d['p50_ms'], d.get('p50_kernels_ms_rank0'))" \
+              "$O/p50lib_${v}_$r.json" "$v"
+        done
+      done ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
