@@ -568,6 +568,10 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
             xk[j] = i < a.cap ? src[i] : kKeyNone;
         }
         const uint32_t cnt = a.cnt[q];
+#ifdef BSR_RESCORE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (lab: the keys' arrival, stamp 5)
+        BSR_STAMP(1, 5);
+#endif
         const bool overflow = cnt > a.cap;
         uint32_t c = overflow ? 0u : cnt;
         float tx = INFINITY;

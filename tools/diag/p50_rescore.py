@@ -55,14 +55,15 @@ print(f"kp={os.environ.get('BSR_RESCORE_KP', '1')} rows {N} queries {Q}: wall me
       flush=True)
 if os.environ.get("BSR_READ_STAMPS") == "1":
     # the lab build's per-query phase stamps of the last search (make lab-stamps; kp kernel:
-    # 0 start, 1 keys + select, 2 rows of chunk 0 in LDS, 3 the 12 chunks walked, 4 finish)
+    # 0 start, 5 keys arrived, 1 select, 2 rows of chunk 0 in LDS, 3 the 12 chunks walked, 4 finish)
     import ctypes
     st = np.zeros((4096, 8), np.uint64)
     L.bsr_lab_rescore_stamps.restype = ctypes.c_int
     assert L.bsr_lab_rescore_stamps(st.ctypes.data_as(ctypes.c_void_p), 4096) == 0
-    s = st[:Q, :5].astype(np.int64)
+    s = st[:Q, :6].astype(np.int64)
     us = (s - s[:, :1]) / 100.0
-    for nm, i in (("keys + select", 1), ("rows -> LDS", 2), ("walk chunks", 3), ("finish", 4)):
-        d = us[:, i] - us[:, i - 1]
+    for nm, i, j in (("keys arrive", 5, 0), ("select", 1, 5), ("rows -> LDS", 2, 1), ("walk chunks", 3, 2),
+                     ("finish", 4, 3)):
+        d = us[:, i] - us[:, j]
         print(f"  {nm:16s} median {np.median(d):7.2f} max {d.max():7.2f} us", flush=True)
     print(f"  {'total':16s} median {np.median(us[:, 4]):7.2f} max {us[:, 4].max():7.2f} us", flush=True)
