@@ -505,7 +505,7 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
         // them once it sees the flag.
         // (a one-workgroup grid -- a tiny batch's second chance -- is its own last arrival: no
         // agent fences, no ticket)
-        const bool solo = gridDim.x == 1;
+        const bool solo = a.solo != 0;
         __shared__ uint32_t s_last;
         __syncthreads();  // (s_wrote final)
         if (!solo && (s_wrote || (!a.hres_idx && blockIdx.x * QPW < n_items))) __threadfence();
@@ -1156,8 +1156,10 @@ extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
 #ifndef BSR_GT_RESCORE_P
 #define BSR_GT_RESCORE_P 2
 #endif
-hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
-    if (!a.n_items) return hipSuccess;
+hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
+    if (!a_in.n_items) return hipSuccess;
+    RescoreArgs a = a_in;
+    a.solo = 0;
     const uint32_t e = (a.k + 63) / 64;
     // the first pass (mode S) of a tiny batch: one workgroup per query, one wave per chunk
     // (BSR_RESCORE_KP=0: the one-wave kernel instead, for A/B runs)
@@ -1174,8 +1176,14 @@ hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s) {
     const bool dev = a.n_items_dev != nullptr;
     // (one item per wave: four independent waves per workgroup, one workgroup per CU)
     // (a tiny batch's second chance: one workgroup, its own last arrival -- rarely any item)
-    const uint32_t gdev = a.n_items <= 16 ? 1u : std::min<uint32_t>(a.n_items, kRescoreAllGrid);
+    // (BSR_SOLO_PUB=0: the grid as before, for A/B runs)
+    static const bool solo_on = [] {
+        const char* v = getenv("BSR_SOLO_PUB");
+        return !(v && v[0] == '0');
+    }();
+    const uint32_t gdev = solo_on && a.n_items <= 16 ? 1u : std::min<uint32_t>(a.n_items, kRescoreAllGrid);
     const dim3 g(dev ? gdev : (a.n_items + 3) / 4), b(dev ? 512 : 256);
+    a.solo = dev && solo_on && a.n_items <= 16 ? 1u : 0u;
 #define BSR_RESCORE(E)                                                                        \
     do {                                                                                      \
         if (dev) hipLaunchKernelGGL((k_rescore<E, 8, 2>), g, b, 0, s, a);                     \

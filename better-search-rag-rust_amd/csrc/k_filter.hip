@@ -10,6 +10,7 @@
 // is k_filter_qs16 (v_mfma_i32_16x16x64_i8, rows of an even number of 64-byte K slices up to
 // 768 bytes); k_filter (v_mfma_i32_32x32x32_i8) serves the other row widths.  (The bf16
 // operand of rounds 1-3 is retired: half the int8 MFMA rate at an equal bound.)
+#include <cstdlib>
 #include "bsr_device.hpp"
 #include "kernels.hpp"
 
@@ -1606,7 +1607,8 @@ __global__ __launch_bounds__(1024) void k_select_tau_m(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < NV; ++j) m = fmaxf(m, v[j]);
     const uint64_t sorted = wave_sort64(score_key(m, (uint32_t)lane));
-    if (lane == 0) lbw[w] = score_key_score(shfl64(sorted, (int)ks - 1));
+    const uint64_t kth = shfl64(sorted, (int)ks - 1);  // (every lane: a shuffle reads active lanes only)
+    if (lane == 0) lbw[w] = score_key_score(kth);
     __syncthreads();
     float lb = lbw[0];
 #pragma unroll
@@ -1801,7 +1803,11 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
                              hipStream_t s, uint64_t* smax) {
     if (ks > 2 * kWave) return hipErrorInvalidValue;
-    if (ks <= kWave && qpad <= 16 && n_s > 16 * kWave && n_s <= 16 * 16 * kWave)
+    static const bool m_on = [] {  // (BSR_SELECT_TAU_M=0: the 4-wave kernel instead, for A/B runs)
+        const char* v = getenv("BSR_SELECT_TAU_M");
+        return !(v && v[0] == '0');
+    }();
+    if (m_on && ks <= kWave && qpad <= 16 && n_s > 16 * kWave && n_s <= 16 * 16 * kWave)
         hipLaunchKernelGGL(k_select_tau_m<16>, dim3(qpad), dim3(1024), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
                            tau, cnt, status, smax);
     else if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)

@@ -208,6 +208,7 @@ struct RescoreArgs {
     size_t pub_bytes;
     uint32_t* pub_flag;
     uint32_t* pub_ticket;       // kTicketWords device words, 0 between launches
+    uint32_t solo;              // (set by launch_rescore) a one-workgroup grid: its own last arrival
 };
 // The publishing kernels' arrival ticket: kTicketLeaves leaf counters and one root counter,
 // each on a 64-byte line of its own (a workgroup adds to its leaf, blockIdx % kTicketLeaves; the

@@ -343,7 +343,11 @@ def test_published_rescue_and_fallback_rows(bsr_mod, oracle_mod, gpu, nq, n_resc
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
     perm = rng.permutation(n)
     at = 0
-    for q, m in [(q, 200) for q in range(n_rescue)] + [(q, 1500) for q in range(n_rescue, n_rescue + n_over)]:
+    # (one query: 120 near-duplicates, so that fewer than ks = 8 of them fall into its every-32nd-row
+    # sample -- with 200, this seed samples enough of them to put tau0 among the duplicates, and the
+    # query legitimately takes the exact scan)
+    m_rescue = 200 if nq > 1 else 120
+    for q, m in [(q, m_rescue) for q in range(n_rescue)] + [(q, 1500) for q in range(n_rescue, n_rescue + n_over)]:
         pos = perm[at:at + m]
         at += m
         rows[pos] = qs[q] + rng.normal(0, 1e-3, (m, dim)).astype(np.float32)

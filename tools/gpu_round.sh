@@ -106,6 +106,21 @@ for step in $STEPS; do
               "$O/p50lib_${v}_$r.json" "$v"
         done
       done ;;
+    c3fb)
+      # the configs[3] searches' stats under the tiny-batch A/B variables (tools/diag/c3_fallback.py)
+      for e in "" "BSR_SELECT_TAU_M=0" "BSR_SOLO_PUB=0" "BSR_SELECT_TAU_M=0 BSR_SOLO_PUB=0"; do
+        env $e timeout -k 10 200 python3 tools/diag/c3_fallback.py >> "$O/c3fb.txt" 2>> "$O/err.txt" || exit 1
+      done
+      cat "$O/c3fb.txt" ;;
+    seltau)
+      timeout -k 10 60 tools/microbench/seltau_ab > "$O/seltau.txt" 2>&1; rc=$?; cat "$O/seltau.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    rescue1)
+      for e in "" "BSR_SOLO_PUB=0" "BSR_SELECT_TAU_M=0" "BSR_RESCORE_KP=0" "BSR_SOLO_PUB=0 BSR_SELECT_TAU_M=0 BSR_RESCORE_KP=0"; do
+        for nq in 1 2; do
+          env $e timeout -k 10 120 python3 tools/diag/rescue1.py $nq >> "$O/rescue1.txt" 2>> "$O/err.txt" || exit 1
+        done
+      done
+      cat "$O/rescue1.txt" ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
