@@ -35,6 +35,13 @@
 #   ab:A,B,...  bench.py A/B of alternative libbsr builds (tools/ab/libbsr_<A>.so; "new" = tree),
 #               interleaved, two rounds; ab125:A,B,... the same at the 1.25M-row shard; abc2 / abc5:
 #               configs[1] (1M x 1000) / the configs[4] shard (6.25M bf16 x 4096, top-100)
+#   p50ab       p50 with the tiny-batch rescore on / off (BSR_RESCORE_KP), interleaved
+#   p50lib:A,B  p50 of one query over 10M rows per libbsr build, interleaved
+#   p50rs       the single-query rescore events (tools/diag/p50_rescore.py), kp on / off
+#   p50st       the tiny-batch rescore's lab stamps + a kernel timeline of single-query searches at 2M rows
+#   seltau      tools/microbench/seltau_ab: k_select_tau_m vs k_select_tau, bit for bit
+#   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
+#   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
 TAG=${1:-run}
 shift
 STEPS=${*:-tests bench}
