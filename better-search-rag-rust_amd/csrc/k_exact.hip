@@ -528,6 +528,146 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
 
 
 // ------------------------------------------------------------------------------------
+// The global threshold's rescore (mode B with exclusion bounds; round 5): four
+// queries per workgroup, their emitted rows DEALT over the workgroup's 256 lanes -- lane t of a
+// round scores row t of the four lists laid end to end -- instead of one query per wave.  A rank
+// emits ~32 rows per query on average, so one query per wave left half its lanes idle while a
+// query with more than 64 rows on this rank ran a second batch of chunks alone and set the
+// kernel's time (median wave 24.6 us, slowest 38.7 us, profiles/r05k_rstamps_gtau.txt); dealt, a
+// workgroup takes one round unless its four queries hold more than 256 rows.  Each lane walks its
+// row against its own query's LDS copy in index order, exactly as k_rescore; the keys of a round go
+// through LDS, and wave w keeps query w's list.  Then wave w finishes query w as k_rescore's
+// global-threshold branch does (the list, the exclusion bound, the result rows).
+// ------------------------------------------------------------------------------------
+template <int E, int NC>
+__global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
+    constexpr int QW = 4, STAGE = 64 * 68, QMAX = 1024, T = 64 * QW;
+    __shared__ __attribute__((aligned(16))) float stage_all[QW * STAGE];
+    __shared__ __attribute__((aligned(16))) float ldq[QW][QMAX];
+    __shared__ uint64_t kbuf[T];
+    __shared__ uint32_t s_c[QW], s_ov[QW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+    float* const lds = stage_all + w * STAGE;
+    if (a.next_status && blockIdx.x == 0 && tid < kWave) {
+        // (k_finalize's bookkeeping, fused, as k_rescore)
+        if (tid < kStWords) a.next_status[tid] = 0;
+        if (a.merge_words && tid < 2) a.merge_words[tid] = tid ? ~0u : 0u;
+        uint32_t sum = 0;
+        for (uint32_t q = tid; q < a.n_queries; q += kWave) sum += a.emit_cnt[q];
+        sum = wave_reduce_u32(sum, [](uint32_t x, uint32_t y) { return x + y; });
+        if (tid == 0) a.cur_status[kStEmitted] = sum;
+    }
+    const uint32_t q0 = blockIdx.x * QW, qw = q0 + w, ld = a.ld, dim = a.dim;
+    const bool has_q = qw < a.n_items;
+    if (lane == 0) {
+        const uint32_t cn = has_q ? a.cnt[qw] : 0u;
+        s_ov[w] = cn > a.cap ? 1u : 0u;  // rows were dropped: nothing can be certified
+        s_c[w] = cn > a.cap ? 0u : cn;
+    }
+    if (has_q) {
+        constexpr int QN = QMAX / 64;
+        const float* qsrc = a.qf32 + (uint64_t)qw * ld;
+        float qv[QN];
+#pragma unroll
+        for (int j = 0; j < QN; ++j) qv[j] = (uint32_t)(j * 64 + lane) < ld ? qsrc[j * 64 + lane] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < QN; ++j)
+            if ((uint32_t)(j * 64 + lane) < ld) ldq[w][j * 64 + lane] = qv[j];
+    }
+    __syncthreads();
+    const uint32_t o1 = s_c[0], o2 = o1 + s_c[1], o3 = o2 + s_c[2], total = o3 + s_c[3];
+    const uint32_t my_lo = w == 0 ? 0u : w == 1 ? o1 : w == 2 ? o2 : o3, my_hi = my_lo + s_c[w];
+    WaveTopK<E> L;
+    L.init();
+    uint64_t thr = kKeyNone;
+    const uint32_t nch = NC ? (uint32_t)NC : ld / 64;
+    for (uint32_t base = 0; base < total; base += T) {
+        if (base + (uint32_t)w * 64 < total) {  // (wave-uniform) this wave has rows this round
+            const uint32_t f = base + tid;
+            const bool live = f < total;
+            const uint32_t j = live ? (f >= o1) + (f >= o2) + (f >= o3) : 0u;
+            const uint32_t qj = q0 + j;
+            const uint32_t lo = j == 0 ? 0u : j == 1 ? o1 : j == 2 ? o2 : o3;
+            const uint32_t myrow = live ? key_row(a.cand_keys[(uint64_t)qj * a.cap + (f - lo)]) : 0u;
+            const float* const qrow = &ldq[j][0];
+            float acc[1] = {-0.0f}, mx[1] = {0.0f};
+            uint32_t lrow[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
+            auto step = [&](f32x4_t (&pre)[16], uint32_t ch, uint32_t ahead) {
+                wave_sync();
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int L16 = i * 64 + lane;
+                    *reinterpret_cast<f32x4_t*>(lds + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
+                }
+                wave_sync();
+                if (ch + ahead < nch) load_cand_chunk(pre, a.rows, ld, lrow, ch + ahead, lane);
+                const float* const bb[1] = {qrow + ch * 64};
+                const uint32_t nvalid = dim - ch * 64 < 64 ? dim - ch * 64 : 64;
+                seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
+            };
+            if constexpr (NC > 0) {
+                f32x4_t pre[2][16];
+                load_cand_chunk(pre[0], a.rows, ld, lrow, 0, lane);
+                if (NC > 1) load_cand_chunk(pre[1], a.rows, ld, lrow, 1, lane);
+#pragma unroll
+                for (uint32_t ch = 0; ch < (uint32_t)NC; ++ch) step(pre[ch % 2], ch, 2);
+            } else {
+                f32x4_t preA[16], preB[16];
+                load_cand_chunk(preA, a.rows, ld, lrow, 0, lane);
+                if (nch > 1) load_cand_chunk(preB, a.rows, ld, lrow, 1, lane);
+                for (uint32_t ch = 0; ch < nch; ch += 2) {
+                    step(preA, ch, 2);
+                    if (ch + 1 < nch) step(preB, ch + 1, 2);
+                }
+            }
+            const float d = finish_distance(acc[0], mx[0], a.na[myrow], a.nb[qj]);
+            kbuf[tid] = live ? dist_key(d, myrow) : kKeyNone;
+        }
+        __syncthreads();
+        // wave w: the keys of query w scored this round
+        const uint32_t lo = my_lo > base ? my_lo : base, hi = my_hi < base + T ? my_hi : base + T;
+        for (uint32_t x = lo; x < hi; x += kWave) {
+            const uint32_t idx = x + lane;
+            L.offer(idx < hi ? kbuf[idx - base] : kKeyNone, (int)a.k, thr);
+        }
+        __syncthreads();  // (kbuf and the stages are the next round's)
+    }
+    if (!has_q) return;
+    const uint32_t q = qw, c = s_c[w];
+    L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
+    if (lane == 0) {
+        // the distance below which no row left out can lie (k_rescore's global-threshold branch)
+        const float mag_b = a.nb[q];
+        const float tx = s_ov[w] ? INFINITY : a.tau0[q];
+        const double eb = (double)a.ebound[q];
+        double x;
+        if (tx == -INFINITY) x = INFINITY;  // every row of the shard was a candidate
+        else if (!(tx < INFINITY) || !(eb < 1.0) || !((double)tx < 1.0 - eb - 1e-4 - 6e-9 / (double)mag_b))
+            x = -INFINITY;
+        else x = 1.0 - (double)tx - eb - 2.5e-7;
+        float xf = (float)x;
+        if ((double)xf > x) xf = nextafterf(xf, -INFINITY);  // (rounded down)
+        a.excl_out[q] = xf;
+    }
+    if (a.res_idx) {
+        const uint32_t cnt = min(a.k, c);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = e * kWave + lane;
+            if (i < a.k) {
+                const uint64_t key = L.v[e];
+                const bool has = i < cnt && key != kKeyNone;
+                a.res_idx[(uint64_t)q * a.k + i] = has ? a.offset + key_row(key) : ~0ull;
+                a.res_dist[(uint64_t)q * a.k + i] = has ? key_dist(key) : INFINITY;
+            }
+        }
+        if (lane == 0) a.res_cnt[q] = cnt;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // The first rescore pass of a tiny batch (<= 16 queries: the single-query p50 path), mode S
 // (round 5): ONE workgroup per query with one wave per 64-float chunk of the rows (ld / 64 <= 16
 // waves).  Wave 0 selects the k' candidates (select_kp); then every wave loads ITS chunk of every
@@ -1170,6 +1310,30 @@ hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && a.n_items <= 16 && a.ld % 64 == 0 &&
         a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && a.cap <= 1024) {
         hipLaunchKernelGGL(k_rescore_kp<1>, dim3(a.n_items), dim3(a.ld), 0, s, a);
+        return hipGetLastError();
+    }
+    // the global threshold's rescore: four queries' rows dealt over a workgroup (BSR_GT_FLAT=0:
+    // one wave per query instead, for A/B runs)
+    static const bool flat_on = [] {
+        const char* v = getenv("BSR_GT_FLAT");
+        return !(v && v[0] == '0');
+    }();
+    if (flat_on && a.excl_out && a.cand_keys && !a.sel && !a.n_items_dev && !a.pub_flag && !a.hres_idx &&
+        !a.qlist && a.ld % 64 == 0 && a.ld <= 1024 && BSR_GT_RESCORE_W == 1) {
+        const dim3 gf((a.n_items + 3) / 4), bf(256);
+#define BSR_FLAT(E)                                                                           \
+    do {                                                                                      \
+        if (a.ld == 768) hipLaunchKernelGGL((k_rescore_flat<E, 12>), gf, bf, 0, s, a);        \
+        else hipLaunchKernelGGL((k_rescore_flat<E, 0>), gf, bf, 0, s, a);                     \
+    } while (0)
+        switch (e) {
+            case 1: BSR_FLAT(1); break;
+            case 2: BSR_FLAT(2); break;
+            case 3: BSR_FLAT(3); break;
+            case 4: BSR_FLAT(4); break;
+            default: return hipErrorInvalidValue;
+        }
+#undef BSR_FLAT
         return hipGetLastError();
     }
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item

@@ -42,6 +42,8 @@
 #   seltau      tools/microbench/seltau_ab: k_select_tau_m vs k_select_tau, bit for bit
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
+#   abflat      the loopback step with the dealt-rows global-threshold rescore on / off (after looprec)
+#   mrall       every multi-rank GPU test (tests/test_gpu_multirank.py, the full-size ones included)
 TAG=${1:-run}
 shift
 STEPS=${*:-tests bench}
@@ -128,6 +130,19 @@ for step in $STEPS; do
         done
       done
       cat "$O/rescue1.txt" ;;
+    abflat)
+      # the loopback step with the dealt-rows global-threshold rescore on / off (BSR_GT_FLAT), interleaved
+      for r in 1 2; do
+        for v in 1 0; do
+          BSR_GT_FLAT=$v run 300 "abflat $v $r" "$O/abflat_${v}_$r.json" python bench.py --comm loopback --gpus 8 \
+              --replay "$O/loop8.npz" --steps 50 --warmup 5 --verify 4 --p50-iters 5 $NOB
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_ms_per_step_rank0']; print('flat', sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['emitted_per_query_rank0'], k['rescore'], d['loopback']['missed_allgathers'], d.get('parity_spot_check'))" \
+              "$O/abflat_${v}_$r.json" "$v"
+        done
+      done ;;
+    mrall)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 300 --timeout-method thread > "$O/pytest_mrall.log" 2>&1
+      rc=$?; echo "pytest mrall rc=$rc"; tail -3 "$O/pytest_mrall.log"; [ $rc -eq 0 ] || exit $rc ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
