@@ -43,6 +43,7 @@
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
 #   abflat      the loopback step with the dealt-rows global-threshold rescore on / off (after looprec)
+#   smoke       __graft_entry__.smoke() (the driver's round-end check)
 #   mrall       every multi-rank GPU test (tests/test_gpu_multirank.py, the full-size ones included)
 TAG=${1:-run}
 shift
@@ -143,6 +144,9 @@ for step in $STEPS; do
     mrall)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 300 --timeout-method thread > "$O/pytest_mrall.log" 2>&1
       rc=$?; echo "pytest mrall rc=$rc"; tail -3 "$O/pytest_mrall.log"; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.txt" 2>&1
+      rc=$?; tail -2 "$O/smoke.txt"; [ $rc -eq 0 ] || exit $rc ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
