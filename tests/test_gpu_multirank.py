@@ -215,6 +215,31 @@ def test_loopback_replicated_matches_own_shard(bsr_mod, oracle_mod, gpu, corpus)
     ix.close()
 
 
+@pytest.mark.parametrize("dim,k", [(200, 10), (200, 70), (64, 33)])
+def test_loopback_global_threshold_other_widths(bsr_mod, oracle_mod, gpu, dim, k):
+    """The global-threshold path (k_rescore_flat's generic-width walk, partial last chunks, lists
+    of more than 64 entries) through a replicating loopback communicator on rows of other widths:
+    the merged lists are the rank's own top-k, bit for bit."""
+    rng = np.random.default_rng(dim * 1000 + k)
+    rows = rng.uniform(-1, 1, (40000, dim)).astype(np.float32)
+    q = rng.uniform(-1, 1, (40, dim)).astype(np.float32)
+    q[0] = rows[7]
+    ix = bsr_mod.Index(dim, max_k=128, device=0)
+    ix.load(rows, 0)
+    comm = bsr_mod.Comm.loopback(0, 8, 0)
+    got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, k)
+    assert ix.last_stats().n_candidates == 0  # (the global-threshold path)
+    wi, wd, wc = oracle_mod.parallel_top_k(rows, q, k, size=4, threads=4)
+    assert np.array_equal(got[2], wc)
+    for j in range(len(q)):
+        c = int(wc[j])
+        assert np.array_equal(got[0][j, :c], wi[j, :c]), j
+        assert np.array_equal(got[1][j, :c].view(np.uint32), wd[j, :c].view(np.uint32)), j
+    assert got[0][0, 0] == 7
+    comm.close()
+    ix.close()
+
+
 def test_loopback_replays_recorded_run(bsr_mod, gpu, corpus, tmp_path):
     """Rank 0 of a real 3-rank run (host transport) records its all-gathers; a loopback
     communicator replaying them on rank 0's shard alone reproduces that run's global result bit
