@@ -1562,11 +1562,13 @@ __global__ __launch_bounds__(256) void k_select_tau_w(const float* __restrict__ 
 }
 
 // The same selection for tiny batches (<= 16 queries: the single-query p50 path) over long sample
-// rows (n_s <= 16 x 64 NV): SIXTEEN waves per query, each holding a sixteenth of the row in
-// registers.  The lower bound lb is the largest of the waves' ks-th lane maxima (each a lower bound
-// of the query's ks-th value, as above); each wave keeps its own ks best among the values >= lb
-// (usually a few), and wave 0 merges the non-empty lists.  Exact, so tau and the ks best keys are
-// k_select_tau's, bit for bit; one 4-wave workgroup per query spent ~20 us at 10M rows.
+// rows (2048 < n_s <= 16 x 64 NV; shorter rows take k_select_tau_w): SIXTEEN waves per query,
+// each holding a sixteenth of the row in registers.  The lower bound lb is the largest of the
+// waves' ks-th lane maxima (each a lower bound of the query's ks-th value, as above); each wave
+// keeps its own ks best among the values >= lb (usually a few), and wave 0 merges the waves' ks
+// best.  Exact, so tau and the ks best keys are k_select_tau's, bit for bit
+// (tools/microbench/seltau_ab); timed alone at one query over 9766 values, 13.8 us for one 4-wave
+// workgroup (tools/microbench/seltau_time).
 template <int NV>
 __global__ __launch_bounds__(1024) void k_select_tau_m(const float* __restrict__ S, uint32_t s_ld, uint32_t n_s,
                                                        uint32_t nq, uint32_t qpad, const uint32_t* __restrict__ qflags,
@@ -1593,8 +1595,6 @@ __global__ __launch_bounds__(1024) void k_select_tau_m(const float* __restrict__
     }
     __shared__ float lbw[NW];
     __shared__ uint64_t part[NW][kWave];
-    __shared__ uint32_t s_has;
-    if (t == 0) s_has = 0;
     const float* s = S + (uint64_t)q * s_ld;
     const uint32_t per = (n_s + NW - 1) / NW, lo = w * per, hi = lo + per < n_s ? lo + per : n_s;
     float v[NV];
@@ -1621,14 +1621,16 @@ __global__ __launch_bounds__(1024) void k_select_tau_m(const float* __restrict__
         const uint32_t i = lo + j * kWave + lane;
         if (lo + j * kWave < hi) L.offer((i < hi && v[j] >= lb) ? score_key(v[j], i) : kKeyNone, (int)ks, thr);
     }
-    part[w][lane] = L.v[0];
-    if (lane == 0 && L.v[0] != kKeyNone) atomicOr(&s_has, 1u << w);
+    // each wave's ks best (the query's ks best are among them), packed [w][ks]: wave 0 merges
+    // 16 ks keys in batches of 64 (two for ks = 8), not sixteen 64-key lists
+    uint64_t* const packed = &part[0][0];
+    if (lane < (int)ks) packed[w * ks + lane] = L.v[0];
     __syncthreads();
     if (w != 0) return;
     WaveTopK<1> M;
     M.init();
     uint64_t mt = kKeyNone;
-    for (uint32_t h = s_has; h; h &= h - 1) M.offer(part[__builtin_ctz(h)][lane], (int)ks, mt);
+    for (uint32_t b = 0; b < NW * ks; b += kWave) M.offer(b + lane < NW * ks ? packed[b + lane] : kKeyNone, (int)ks, mt);
     if (lane == 0) tau[q] = score_key_score(mt);
     if (smax) M.store(smax + (uint64_t)q * ks, (int)ks);
 }
@@ -1807,7 +1809,7 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
         const char* v = getenv("BSR_SELECT_TAU_M");
         return !(v && v[0] == '0');
     }();
-    if (m_on && ks <= kWave && qpad <= 16 && n_s > 16 * kWave && n_s <= 16 * 16 * kWave)
+    if (m_on && ks <= kWave && qpad <= 16 && n_s > 32 * kWave && n_s <= 16 * 16 * kWave)
         hipLaunchKernelGGL(k_select_tau_m<16>, dim3(qpad), dim3(1024), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
                            tau, cnt, status, smax);
     else if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)

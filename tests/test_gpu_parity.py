@@ -83,7 +83,8 @@ def test_golden_search(bsr_mod, gpu, exact_only):
     (1, 768, 1, 10), (5, 768, 3, 10), (257, 768, 2, 1), (1000, 768, 5, 64), (3000, 130, 9, 100),
     (4097, 768, 4, 256), (20000, 768, 8, 50), (100000, 768, 16, 10), (70000, 96, 1, 10),
     (3000, 130, 9, 10), (8000, 200, 3, 5), (50000, 1024, 2, 10),
-    (1200000, 128, 3, 10)])  # (1172 compact sample maxima: the 16-wave tau selection)
+    (1200000, 128, 3, 10),   # (1172 compact sample maxima: one wave per query selects tau)
+    (2200000, 64, 2, 10)])   # (2149 maxima: the 16-wave tau selection, k_select_tau_m)
 def test_small_batches_vs_oracle(bsr_mod, oracle_mod, gpu, n, dim, nq, k):
     rng = np.random.default_rng(n + dim + k)
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)

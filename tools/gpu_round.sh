@@ -123,7 +123,8 @@ for step in $STEPS; do
       done
       cat "$O/c3fb.txt" ;;
     seltau)
-      timeout -k 10 60 tools/microbench/seltau_ab > "$O/seltau.txt" 2>&1; rc=$?; cat "$O/seltau.txt"; [ $rc -eq 0 ] || exit $rc ;;
+      timeout -k 10 60 tools/microbench/seltau_ab > "$O/seltau.txt" 2>&1; rc=$?; cat "$O/seltau.txt"; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 60 tools/microbench/seltau_time > "$O/seltau_time.txt" 2>&1; rc=$?; cat "$O/seltau_time.txt"; [ $rc -eq 0 ] || exit $rc ;;
     rescue1)
       for e in "" "BSR_SOLO_PUB=0" "BSR_SELECT_TAU_M=0" "BSR_RESCORE_KP=0" "BSR_SOLO_PUB=0 BSR_SELECT_TAU_M=0 BSR_RESCORE_KP=0"; do
         for nq in 1 2; do
