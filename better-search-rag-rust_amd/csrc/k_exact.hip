@@ -539,6 +539,9 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
 // through LDS, and wave w keeps query w's list.  Then wave w finishes query w as k_rescore's
 // global-threshold branch does (the list, the exclusion bound, the result rows).
 // ------------------------------------------------------------------------------------
+#ifndef BSR_GT_FLAT_P
+#define BSR_GT_FLAT_P 2
+#endif
 template <int E, int NC>
 __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
     constexpr int QW = 4, STAGE = 64 * 68, QMAX = 1024, T = 64 * QW;
@@ -608,11 +611,13 @@ __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
                 seq_chunk<1>(lds + lane * 68, bb, nvalid, acc, mx);
             };
             if constexpr (NC > 0) {
-                f32x4_t pre[2][16];
-                load_cand_chunk(pre[0], a.rows, ld, lrow, 0, lane);
-                if (NC > 1) load_cand_chunk(pre[1], a.rows, ld, lrow, 1, lane);
+                // BSR_GT_FLAT_P chunks of loads in flight (a register ring)
+                constexpr uint32_t PP = (uint32_t)BSR_GT_FLAT_P < (uint32_t)NC ? (uint32_t)BSR_GT_FLAT_P : (uint32_t)NC;
+                f32x4_t pre[PP][16];
 #pragma unroll
-                for (uint32_t ch = 0; ch < (uint32_t)NC; ++ch) step(pre[ch % 2], ch, 2);
+                for (uint32_t ch = 0; ch < PP; ++ch) load_cand_chunk(pre[ch], a.rows, ld, lrow, ch, lane);
+#pragma unroll
+                for (uint32_t ch = 0; ch < (uint32_t)NC; ++ch) step(pre[ch % PP], ch, PP);
             } else {
                 f32x4_t preA[16], preB[16];
                 load_cand_chunk(preA, a.rows, ld, lrow, 0, lane);
