@@ -225,6 +225,61 @@ __device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c,
     wave_sync();
 }
 
+// Certification: every row outside the candidate set has approximate cosine
+// <= tau_x, hence reference cosine <= tau_x + E_q and reference distance >= 1 - tau_x - E_q -
+// 2^-23; the k-th exact distance (key thr) must lie strictly below that, and no excluded row can
+// be element-wise identical to the query.  tau_x = -inf: every row of the shard was a candidate.
+__device__ __forceinline__ bool certify(float tx, uint64_t thr, float ebound_q, float mag_b) {
+    const double ebound = (double)ebound_q;
+    if (tx == -INFINITY) return true;
+    if (!(tx < INFINITY) || thr == kKeyNone) return false;
+    const double dk = (double)key_dist(thr);
+    return ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
+           (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
+}
+// The global threshold's exclusion bound of one rank's list: the distance below
+// which no row it left out can lie, 1 - tau0 - E_q - 2.5e-7 rounded down; +inf when every row of
+// the shard was a candidate, -inf when nothing can be certified.
+__device__ __forceinline__ float exclusion_bound(float tx, float ebound_q, float mag_b) {
+    const double eb = (double)ebound_q;
+    double x;
+    if (tx == -INFINITY) x = INFINITY;
+    else if (!(tx < INFINITY) || !(eb < 1.0) || !((double)tx < 1.0 - eb - 1e-4 - 6e-9 / (double)mag_b))
+        x = -INFINITY;
+    else x = 1.0 - (double)tx - eb - 2.5e-7;
+    float xf = (float)x;
+    if ((double)xf > x) xf = nextafterf(xf, -INFINITY);  // (rounded down)
+    return xf;
+}
+// A query's list (one wave, WaveTopK order) as its first `cnt` result rows (global index,
+// distance), the rest (~0, +inf), and its count -- in device memory and, when the launch has one,
+// the pinned host mirror too.  Returns whether host-mirror rows were written (to be released).
+template <int E>
+__device__ __forceinline__ bool put_result_rows(const RescoreArgs& a, uint32_t q, const WaveTopK<E>& L, uint32_t cnt,
+                                                int lane) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = e * kWave + lane;
+        if (i < a.k) {
+            const uint64_t key = L.v[e];
+            const bool has = i < cnt && key != kKeyNone;
+            const uint64_t gi = has ? a.offset + key_row(key) : ~0ull;
+            const float gd = has ? key_dist(key) : INFINITY;
+            a.res_idx[(uint64_t)q * a.k + i] = gi;
+            a.res_dist[(uint64_t)q * a.k + i] = gd;
+            if (a.hres_idx) {
+                host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
+                host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
+            }
+        }
+    }
+    if (lane == 0) {
+        a.res_cnt[q] = cnt;
+        if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
+    }
+    return a.hres_idx != nullptr || a.hres_cnt != nullptr;
+}
+
 // W waves per workgroup, one query per workgroup at a time: wave w takes candidates
 // w*64 + lane, + 64W, ...; the W per-wave lists merge through LDS.  W = 1: one wave per
 // query (the k' selected candidates, every query).  W = 8: the queries that failed
@@ -422,37 +477,11 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
             bool certified = false;
             if (a.excl_out) {
                 // (global threshold: the root certifies; this rank reports its exclusion bound)
-                if (lane == 0) {
-                    const float tx = overflow ? INFINITY : a.tau0[q];
-                    const double eb = (double)a.ebound[q];
-                    double x;
-                    if (tx == -INFINITY) x = INFINITY;  // every row of the shard was a candidate
-                    else if (!(tx < INFINITY) || !(eb < 1.0) || !((double)tx < 1.0 - eb - 1e-4 - 6e-9 / (double)mag_b))
-                        x = -INFINITY;
-                    else x = 1.0 - (double)tx - eb - 2.5e-7;
-                    float xf = (float)x;
-                    if ((double)xf > x) xf = nextafterf(xf, -INFINITY);  // (rounded down)
-                    a.excl_out[q] = xf;
-                }
+                if (lane == 0) a.excl_out[q] = exclusion_bound(overflow ? INFINITY : a.tau0[q], a.ebound[q], mag_b);
             } else if (lane == 0) {
-                // Certification: every row outside the candidate set has
-                // approximate cosine <= tau_x, hence reference cosine <= tau_x + E_q and
-                // reference distance >= 1 - tau_x - E_q - 2^-23; the k-th exact distance must
-                // lie strictly below that, and no excluded row can be element-wise identical to
-                // the query.  Mode B: every emitted row is a candidate, so tau_x is the
-                // emission threshold tau0.
+                // (mode B: every emitted row is a candidate, so tau_x is the emission threshold tau0)
                 const float tx = overflow ? INFINITY : sel ? tx_sel : (all ? a.tau0[q] : a.tau_excl[q]);
-                const double ebound = (double)a.ebound[q];
-                bool ok;
-                if (tx == -INFINITY) {
-                    ok = true;  // every row of the shard was a candidate
-                } else if (!(tx < INFINITY) || thr == kKeyNone) {
-                    ok = false;
-                } else {
-                    const double dk = (double)key_dist(thr);
-                    ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
-                         (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
-                }
+                const bool ok = certify(tx, thr, a.ebound[q], mag_b);
                 if (!ok) {
                     const uint32_t pos = atomicAdd(a.fail_cnt, 1u);
                     a.fail_list[pos] = q;
@@ -464,28 +493,7 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
             // B) become result rows now; the first pass's uncertified ones are left to mode B
             if (a.res_idx && (W > 1 || a.excl_out || __shfl((int)certified, 0, kWave))) {
                 const uint32_t cnt = a.excl_out ? min(a.k, c) : (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const uint32_t i = e * kWave + lane;
-                    if (i < a.k) {
-                        const uint64_t key = L.v[e];
-                        const bool has = i < cnt && key != kKeyNone;
-                        const uint64_t gi = has ? a.offset + key_row(key) : ~0ull;
-                        const float gd = has ? key_dist(key) : INFINITY;
-                        a.res_idx[(uint64_t)q * a.k + i] = gi;
-                        a.res_dist[(uint64_t)q * a.k + i] = gd;
-                        if (a.hres_idx) {
-                            host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
-                            host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
-                            host_rows = true;
-                        }
-                    }
-                }
-                if (lane == 0) {
-                    a.res_cnt[q] = cnt;
-                    if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
-                }
-                host_rows = host_rows || a.hres_cnt != nullptr;
+                host_rows = put_result_rows(a, q, L, cnt, lane) || host_rows;
             }
         }
         BSR_STAMP(W, 4);
@@ -642,34 +650,8 @@ __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
     if (!has_q) return;
     const uint32_t q = qw, c = s_c[w];
     L.store(a.out_keys + (uint64_t)q * a.k, (int)a.k);
-    if (lane == 0) {
-        // the distance below which no row left out can lie (k_rescore's global-threshold branch)
-        const float mag_b = a.nb[q];
-        const float tx = s_ov[w] ? INFINITY : a.tau0[q];
-        const double eb = (double)a.ebound[q];
-        double x;
-        if (tx == -INFINITY) x = INFINITY;  // every row of the shard was a candidate
-        else if (!(tx < INFINITY) || !(eb < 1.0) || !((double)tx < 1.0 - eb - 1e-4 - 6e-9 / (double)mag_b))
-            x = -INFINITY;
-        else x = 1.0 - (double)tx - eb - 2.5e-7;
-        float xf = (float)x;
-        if ((double)xf > x) xf = nextafterf(xf, -INFINITY);  // (rounded down)
-        a.excl_out[q] = xf;
-    }
-    if (a.res_idx) {
-        const uint32_t cnt = min(a.k, c);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t i = e * kWave + lane;
-            if (i < a.k) {
-                const uint64_t key = L.v[e];
-                const bool has = i < cnt && key != kKeyNone;
-                a.res_idx[(uint64_t)q * a.k + i] = has ? a.offset + key_row(key) : ~0ull;
-                a.res_dist[(uint64_t)q * a.k + i] = has ? key_dist(key) : INFINITY;
-            }
-        }
-        if (lane == 0) a.res_cnt[q] = cnt;
-    }
+    if (lane == 0) a.excl_out[q] = exclusion_bound(s_ov[w] ? INFINITY : a.tau0[q], a.ebound[q], a.nb[q]);
+    if (a.res_idx) put_result_rows(a, q, L, min(a.k, c), lane);  // (no host mirror on this path)
 }
 
 // ------------------------------------------------------------------------------------
@@ -817,47 +799,13 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     bool certified = false;
     if (lane == 0) {
         // certification, as k_rescore mode S
-        const float tx = s_ov ? INFINITY : s_tx;
-        const double ebound = (double)a.ebound[q];
-        bool ok;
-        if (tx == -INFINITY) {
-            ok = true;
-        } else if (!(tx < INFINITY) || thr == kKeyNone) {
-            ok = false;
-        } else {
-            const double dk = (double)key_dist(thr);
-            ok = ebound < 1.0 && dk < 1.0 - (double)tx - ebound - 2.5e-7 &&
-                 (double)tx < 1.0 - ebound - 1e-4 - 6e-9 / (double)mag_b;
-        }
+        const bool ok = certify(s_ov ? INFINITY : s_tx, thr, a.ebound[q], mag_b);
         if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
         certified = ok;
     }
     bool host_rows = false;
-    if (a.res_idx && __shfl((int)certified, 0, kWave)) {
-        const uint32_t cnt = (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t i = e * kWave + lane;
-            if (i < a.k) {
-                const uint64_t key = L.v[e];
-                const bool has = i < cnt && key != kKeyNone;
-                const uint64_t gi = has ? a.offset + key_row(key) : ~0ull;
-                const float gd = has ? key_dist(key) : INFINITY;
-                a.res_idx[(uint64_t)q * a.k + i] = gi;
-                a.res_dist[(uint64_t)q * a.k + i] = gd;
-                if (a.hres_idx) {
-                    host_put(a.hres_idx + (uint64_t)q * a.k + i, gi);
-                    host_put(a.hres_dist + (uint64_t)q * a.k + i, gd);
-                    host_rows = true;
-                }
-            }
-        }
-        if (lane == 0) {
-            a.res_cnt[q] = cnt;
-            if (a.hres_cnt) host_put(a.hres_cnt + q, cnt);
-        }
-        host_rows = host_rows || a.hres_cnt != nullptr;
-    }
+    if (a.res_idx && __shfl((int)certified, 0, kWave))
+        host_rows = put_result_rows(a, q, L, (uint64_t)a.k < a.n_rows ? a.k : (uint32_t)a.n_rows, lane);
     // (the first pass: the host reads these rows once the batch's last kernel raises its flag)
     if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();
     BSR_STAMP(1, 4);
