@@ -1760,7 +1760,7 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 // kernel; other widths: k_filter.  (A one-wave-per-SIMD variant
 // with 64 queries per wave, tools/microbench/k_qs64_lab.hip, measured slower: DESIGN.md §5.)
 // Whether any workgroup of the emit filter can run in a row-stream gang (k_filter_qs16's `gang`
-// condition with its longest static stream).  Otherwise -- every shard of up to ~2.4M rows at 1000
+// condition with its longest static stream).  Otherwise -- every shard of up to ~5.6M rows at 1000
 // queries, and configs[4]'s 16 query tiles -- the launch takes the small-shard build: no gang code
 // (GANG = 0), one tail counter per query tile (TAILX = 0), level 2's bool-array form (L2 = 1) and
 // no explicit wait in the flush (FW = 0): 3-4% faster than the gang build at 1M and 1.25M rows

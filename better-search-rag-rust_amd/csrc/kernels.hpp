@@ -108,7 +108,11 @@ constexpr uint32_t kTailCounters = 64;
 // n_qt <= 4 workgroups' static tile counts, 16 bits each) after the tail counters,
 // cnt[qpad + 8 * kTailCounters ...], zeroed with them.
 constexpr uint32_t kGangWords = 2 * 256;
-constexpr uint32_t kGangMinTiles = 256;  // (static tiles per row stream: ~2.5M rows and up)
+// (static tiles per row stream: gangs from ~5.6M rows at 1000 queries.  Round 5, the filter
+// builds in one process at the global threshold's rate: the gang build 2.4% slower than the
+// small-shard build at 2.5M rows, 0.8% at 5M, 0-1% faster at 10M -- profiles/r05hm_hist_*,
+// r05e_hist_10m.txt; the threshold was 256, ~2.5M rows)
+constexpr uint32_t kGangMinTiles = 600;
 // e0 / e1 (optional): events recorded at the kernel's own dispatch and completion
 // (hipExtLaunchKernel), i.e. its device duration without the stream's launch gaps.
 hipError_t launch_filter_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,

@@ -43,6 +43,7 @@
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
 #   abflat      the loopback step with the dealt-rows global-threshold rescore on / off (after looprec)
+#   histmid     filter_hist at the 5M / 2.5M rank shards (N = 2 / 4) at the global threshold's rate
 #   smoke       __graft_entry__.smoke() (the driver's round-end check)
 #   mrall       every multi-rank GPU test (tests/test_gpu_multirank.py, the full-size ones included)
 TAG=${1:-run}
@@ -148,6 +149,11 @@ for step in $STEPS; do
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.txt" 2>&1
       rc=$?; tail -2 "$O/smoke.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    histmid)
+      # the emit filter builds at the N = 2 / N = 4 rank shards at the global threshold's rate
+      run 300 "filter_hist 5M gtau" "$O/hist_5m_g.txt" tools/microbench/filter_hist 5000000 1000 12 0.1473
+      run 300 "filter_hist 2.5M gtau" "$O/hist_25m_g.txt" tools/microbench/filter_hist 2500000 1000 15 0.1473
+      grep -h -E "median|DIFFER" "$O"/hist_*.txt ;;
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
