@@ -129,6 +129,8 @@ struct bsr_comm {
     bool lb_search = false, lb_live = false;
     int32_t lb_nq = -1, lb_k = -1;  // the recorded search's batch shape (its header): replayed only for it
     uint64_t lb_replayed = 0, lb_missed = 0;
+    uint64_t lb_qdigest = 0;  // FNV-1a of the first host query batch replayed
+    bool lb_qdigest_set = false;
     ~bsr_comm() {
         if (h_mres) (void)hipHostFree(h_mres);
         if (h_flag) (void)hipHostFree(h_flag);
@@ -709,7 +711,7 @@ int bsr_gather_global_top_k(bsr_comm* comm, const uint64_t* local_idx, const flo
 // first header all-gather of a search fails before it is posted, as a buffer that cannot be
 // sized would make it fail; the rank must then post it again with its error status.
 static bool inject_header_fault(const bsr_comm* c) {
-    static const char* v = getenv("BSR_INJECT_FAULT");
+    const char* v = getenv("BSR_INJECT_FAULT");  // (read per search: tests set it in-process)
     if (!v || strncmp(v, "header_hook", 11) != 0) return false;
     return v[11] != ':' || atoi(v + 12) == c->rank;
 }
@@ -826,12 +828,17 @@ static int gtau_reserve(bsr_comm* c, const bsr_index* ix, uint32_t nq, uint32_t 
     BSR_TRY(c->m_res.ensure(mbytes));
     if (c->host_fn) BSR_TRY(c->h_stage.resize(std::max(kb, rbytes) * (1 + P)));
     // (the uncertified queries' staging: sized now, so that no allocation can fail between the
-    // merge and the fallback's collectives)
-    c->f_q.reserve((size_t)nq * ix->dim);
-    c->f_idx.reserve((size_t)nq * k);
-    c->f_dist.reserve((size_t)nq * k);
-    c->f_cnt.reserve(nq);
-    c->f_list.reserve(nq);
+    // merge and the fallback's collectives; bad_alloc becomes an error return, which takes the
+    // rank off the path through its header instead of past it to BSR_GUARD -- ADVICE r05)
+    try {
+        c->f_q.reserve((size_t)nq * ix->dim);
+        c->f_idx.reserve((size_t)nq * k);
+        c->f_dist.reserve((size_t)nq * k);
+        c->f_cnt.reserve(nq);
+        c->f_list.reserve(nq);
+    } catch (const std::bad_alloc&) {
+        return set_error(BSR_E_NOMEM, "host allocation of the fallback staging failed");
+    }
     if (c->h_mres_bytes < mbytes) {
         if (c->h_mres) BSR_HIP(hipHostFree(c->h_mres));
         c->h_mres = nullptr;
@@ -862,10 +869,17 @@ static int gtau_reserve(bsr_comm* c, const bsr_index* ix, uint32_t nq, uint32_t 
 //   4. F (usually empty) takes the standard parallel search (local certified searches, their
 //      exchange and merge), collectively, and its rows replace the root's.
 // RCCL: every step is enqueued behind phase A on the index's stream, one host wait at the end.
+// `a_err` != BSR_OK: this rank's phase A failed after its header put it on the path.
+// It still takes part in every collective, poisoned: no sample keys (kKeyNone) and an empty result
+// whose exclusion bounds are NaN, so that no merged list certifies and every query takes step 4,
+// the standard collective search (where this rank searches again, or contributes an empty list).
+// A non-root rank then returns a_err; the root returns the fallback's status, its rows complete.
 static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint32_t nq, uint32_t k,
-                         uint64_t* out_idx, float* out_dist, uint32_t* out_count) {
+                         uint64_t* out_idx, float* out_dist, uint32_t* out_count, int a_err,
+                         const std::string& a_msg) {
     const uint32_t P = (uint32_t)c->size;
     const bool root = c->rank == 0;
+    const bool poisoned = a_err != BSR_OK;
     hipStream_t s = ix->stream;
     uint64_t n_total = 0;
     for (int32_t r = 0; r < c->size; ++r) {
@@ -874,18 +888,29 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     }
     uint32_t need = (uint64_t)k < n_total ? k : (uint32_t)n_total;
     {  // (test hook, BSR_INJECT_FAULT=gtau_uncertified: no merged list certifies -- F is every query)
-        static const char* v = getenv("BSR_INJECT_FAULT");
+        const char* v = getenv("BSR_INJECT_FAULT");
         if (v && strcmp(v, "gtau_uncertified") == 0) need = k + 1;
     }
     BSR_HIP(hipSetDevice(ix->device));
     // 1. the sample keys of every rank, then phase B
     const size_t kb = (size_t)ix->gt_qpad * ix->gt_ks * sizeof(uint64_t);
-    BSR_TRY(allgather_device(c, ix->smax.p, c->g_smax.p, kb, s));
-    // (phase B's rescore also sets the merge's fail count and NaN word in m_res: two memset
-    // launches fewer on the critical path)
-    BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P, c->m_res.as<uint32_t>()));
-    // 2. the packed result buffers
     const size_t rbytes = ix->res_bytes;
+    if (poisoned) BSR_HIP(hipMemsetAsync(ix->smax.p, 0xff, kb, s));  // (kKeyNone: no sample keys)
+    BSR_TRY(allgather_device(c, ix->smax.p, c->g_smax.p, kb, s));
+    if (!poisoned) {
+        // (phase B's rescore also sets the merge's fail count and NaN word in m_res: two memset
+        // launches fewer on the critical path)
+        BSR_TRY(ix->gtau_phase_b(c->g_smax.as<uint64_t>(), P, c->m_res.as<uint32_t>()));
+    } else {
+        // an empty, uncertifiable contribution: status words and counts 0, exclusion bounds NaN;
+        // the merge's fail count 0 and NaN word ~0 (what phase B's rescore would have set)
+        uint8_t* rb = ix->res[ix->cur].as<uint8_t>();
+        BSR_HIP(hipMemsetAsync(rb, 0, rbytes, s));
+        BSR_HIP(hipMemsetAsync(rb + ix->res_off_x, 0xff, (size_t)nq * sizeof(float), s));
+        BSR_HIP(hipMemsetAsync(c->m_res.p, 0, sizeof(uint32_t), s));
+        BSR_HIP(hipMemsetAsync(c->m_res.as<uint8_t>() + sizeof(uint32_t), 0xff, sizeof(uint32_t), s));
+    }
+    // 2. the packed result buffers
     BSR_TRY(allgather_device(c, ix->res[ix->cur].p, c->g_res.p, rbytes, s));
     // 3. merge + certify into m_res (mres_layout)
     const size_t nqk = (size_t)nq * k;
@@ -934,6 +959,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         d_oc = static_cast<uint32_t*>(coherent_host_alias(out_count));
     }
     const bool direct = d_oi && d_od && d_oc;
+    const uint32_t path = BSR_PATH_COLLECTIVE | BSR_PATH_GLOBAL_TAU | (root && direct ? BSR_PATH_DIRECT_OUT : 0u);
     if (root) {
         ma.hout_idx = direct ? d_oi : reinterpret_cast<uint64_t*>(c->h_mres_dev + o_idx);
         ma.hout_dist = direct ? d_od : reinterpret_cast<float*>(c->h_mres_dev + o_dist);
@@ -960,6 +986,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // 4. the uncertified queries, collectively (every rank holds the same F)
     const uint32_t nf = hw[0];
     ix->stats.n_fallback = nf;
+    ix->stats.parallel_path = path;
     uint32_t* m_cnt = direct ? out_count : reinterpret_cast<uint32_t*>(hm + o_cnt);
     float* m_dist = direct ? out_dist : reinterpret_cast<float*>(hm + o_dist);
     uint64_t* m_idx = direct ? out_idx : reinterpret_cast<uint64_t*>(hm + o_idx);
@@ -994,7 +1021,13 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         ix->stats.n_candidates = 0;  // (this search's path: every emitted row rescored)
         ix->stats.n_fallback = nf;
         ix->stats.n_queries = nq;
+        ix->stats.parallel_path = path | BSR_PATH_FALLBACK;
+        if (poisoned && !root) return set_error(a_err, "%s", a_msg.c_str());
         if (staged != BSR_OK && !root) return set_error(staged, "%s", staged_err.c_str());
+        // (the root's staging failed: its fallback search had no queries; report the real cause)
+        if (staged != BSR_OK && fr == BSR_PARTIAL)
+            set_error(BSR_PARTIAL, "this rank's local search failed (%s); the result covers the other ranks' blocks",
+                      staged_err.c_str());
         // a root whose own fallback search failed still has the other ranks' rows (BSR_PARTIAL):
         // they are patched in and the merged result is handed out with that status
         if (fr != BSR_OK && !(root && fr == BSR_PARTIAL)) return fr;
@@ -1006,6 +1039,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
                 memcpy(m_dist + (size_t)q * k, c->f_dist.data() + (size_t)i * k, k * sizeof(float));
             }
     }
+    if (poisoned && !root) return set_error(a_err, "%s", a_msg.c_str());
     if (!root) return clear_counts(out_count, nq);
     if (direct) return fr;  // (the merged rows, and any fallback rows patched above, are in out_*)
     if (is_device_ptr(out_idx) || is_device_ptr(out_dist) || is_device_ptr(out_count)) {
@@ -1018,6 +1052,25 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         memcpy(out_count, m_cnt, (size_t)nq * sizeof(uint32_t));
     }
     return fr;  // (BSR_OK, or BSR_PARTIAL with bsr_last_error() from the fallback)
+}
+
+// Test switch (BSR_FORCE_COLLECTIVES=1, read per search): a one-rank communicator takes the
+// multi-rank branch, so a one-rank RCCL communicator runs every collective of the parallel search
+// -- the header all-gather on the communicator's stream, the global threshold's key and result
+// all-gathers on the index's stream, the standard path's group of three -- through real RCCL.
+static bool force_collectives() {
+    const char* v = getenv("BSR_FORCE_COLLECTIVES");
+    return v && v[0] == '1';
+}
+
+// Fault injection for the collective-safety tests (BSR_INJECT_FAULT=phase_a0[:rank] or
+// phase_a1[:rank]): the global-threshold search's phase A fails in its first part (before the
+// header) or its second (after it).
+static bool inject_phase_a_fault(const bsr_comm* c, int part) {
+    const char* v = getenv("BSR_INJECT_FAULT");
+    const char* want = part == 0 ? "phase_a0" : "phase_a1";
+    if (!v || strncmp(v, want, 8) != 0) return false;
+    return v[8] != ':' || atoi(v + 9) == c->rank;
 }
 
 // parallel_top_k_similarity_search (src/mpi_helpers/metrics.rs:174-206).  Collective-safe:
@@ -1042,15 +1095,13 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     else if (root && !outs_ok) st = set_error(BSR_E_INVALID, "null output");
     else if (c && !c->host_fn && c->device != ix->device)
         st = set_error(BSR_E_INVALID, "communicator and index on different devices");
-    const bool multi = c && c->size > 1;
+    const bool multi = c && (c->size > 1 || force_collectives());
     bool searched = false;
     if (multi) {
         // global threshold: this rank's filter path with a sample pass, lists the device merge
         // takes, and the library setting (BSR_GLOBAL_TAU=0 turns it off)
-        static const bool gtau_on = [] {
-            const char* v = getenv("BSR_GLOBAL_TAU");
-            return !(v && v[0] == '0');
-        }();
+        const char* gv = getenv("BSR_GLOBAL_TAU");  // (read per search, as the test switches)
+        const bool gtau_on = !(gv && gv[0] == '0');
         // (batches of <= 16 queries -- the latency path -- keep the per-rank threshold: their
         // emission is light, and the standard path overlaps the header with the search)
         bool gt = allow_gtau && gtau_on && st == BSR_OK && nq > kSkinnyMaxQ && ix->gtau_eligible(nq, k) &&
@@ -1065,19 +1116,33 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         c->hdr_posted = false;
         const uint64_t n_rows = ix ? ix->n : 0;
         int lerr = BSR_OK;
+        int a_err = BSR_OK;  // phase A's second part failed after a header that put this rank on the path
+        std::string a_msg;
         if (gt) {
             // the query prep, then the header, then the rest of phase A: the GPU starts on the prep
             // while the host issues the header's launches, and the header's round trip (to the
             // transport and back to the host, which enqueues phase B when it has it) overlaps phase A
-            // instead of following it.  (Enqueue only, every buffer sized: a failure here is a device
-            // error -- fatal to the job, as any device error inside a collective is.)
-            BSR_TRY(ix->gtau_phase_a(queries, 0));
+            // instead of following it.  A failure of the prep (e.g. staging pageable host queries)
+            // goes into the header, which takes every rank off the path.
+            const int ra = inject_phase_a_fault(c, 0)
+                               ? set_error(BSR_E_HIP, "injected fault: phase A, query prep (BSR_INJECT_FAULT)")
+                               : ix->gtau_phase_a(queries, 0);
+            if (ra != BSR_OK) {
+                st = ra;
+                gt = false;
+            }
+        }
+        if (gt) {
             BSR_TRY(post_header(c, nq, k, st, true, n_rows, &lerr));  // (a transport error: every rank sees it)
             if (lerr != BSR_OK) {  // reposted with the failure: this rank, so every rank, is off the path
                 st = lerr;
                 gt = false;
             } else {
-                BSR_TRY(ix->gtau_phase_a(queries, 1));
+                // (past the header: a failure here keeps this rank in every collective, poisoned)
+                a_err = inject_phase_a_fault(c, 1)
+                            ? set_error(BSR_E_HIP, "injected fault: phase A, sample pass (BSR_INJECT_FAULT)")
+                            : ix->gtau_phase_a(queries, 1);
+                if (a_err != BSR_OK) a_msg = last_error_cstr();
             }
         }
         if (!gt) {
@@ -1124,8 +1189,12 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
                                  h0[0], h0[1], r, hr[0], hr[1]);
             all_gt &= hr[4] == 1 && hr[2] == BSR_OK;
         }
-        if (gt && all_gt) return parallel_gtau(c, ix, queries, nq, k, out_idx, out_dist, out_count);
-        if (gt) BSR_HIP(stream_wait(ix->stream));  // (phase A ran for nothing: the standard path)
+        if (gt && all_gt)
+            return parallel_gtau(c, ix, queries, nq, k, out_idx, out_dist, out_count, a_err, a_msg);
+        if (gt) {  // (phase A ran for nothing: the standard path; a failed phase A, an empty contribution)
+            if (a_err != BSR_OK) st = set_error(a_err, "%s", a_msg.c_str());
+            else if (stream_wait(ix->stream) != hipSuccess) st = set_error(BSR_E_HIP, "phase A failed on the device");
+        }
     }
     // compute_local_top_k (:185-191)
     if (st == BSR_OK && !searched) st = ix->search_device(queries, nq, k);
@@ -1160,6 +1229,7 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // succeeded, i.e. that buffer is sized for this batch; host transport: the root's lists
     // come up to its GPU for the same merge)
     const bool dev_merge = ok && device_merge_fits((uint32_t)c->size, k, k);
+    if (ix) ix->stats.parallel_path = BSR_PATH_COLLECTIVE | (root && dev_merge ? BSR_PATH_DEVICE_MERGE : 0u);
     hipStream_t xs = c->host_fn ? nullptr : (ok ? ix->stream : c->stream);
     BSR_TRY(exchange_lists(c, li, ld, lc, !ok, nq, k, xs, !dev_merge || c->host_fn));
     if (ok) bsr_index_collect_profile_impl(ix);
@@ -1188,6 +1258,23 @@ static int parallel_top(bsr_comm* c, bsr_index* ix, const float* queries, uint32
         c->lb_search = true;
         c->lb_live = c->lb_nq == (int32_t)nq && c->lb_k == (int32_t)k;  // (another batch shape: replicate)
         c->lb_cursor = 0;
+        // The replayed contributions are the other ranks' for the RECORDED query batch: replay is
+        // valid only for that batch.  Host batches are checked by digest against the first one
+        // replayed (another batch: a miss, replicated); device batches are taken on trust (the
+        // bench's loopback step replays its one recorded batch).
+        if (c->lb_live && !c->lb_bytes.empty() && queries && !is_device_ptr(queries)) {
+            uint64_t h = 1469598103934665603ull;
+            const uint8_t* b = reinterpret_cast<const uint8_t*>(queries);
+            const size_t nb = (size_t)nq * (ix ? ix->dim : 0) * sizeof(float);
+            for (size_t i = 0; i < nb; ++i) h = (h ^ b[i]) * 1099511628211ull;
+            if (!c->lb_qdigest_set) {
+                c->lb_qdigest = h;
+                c->lb_qdigest_set = true;
+            } else if (h != c->lb_qdigest) {
+                c->lb_live = false;
+                ++c->lb_missed;
+            }
+        }
     }
     const int r = parallel_impl(c, ix, queries, nq, k, out_idx, out_dist, out_count, true);
     if (c) c->lb_search = false;

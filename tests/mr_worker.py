@@ -13,6 +13,10 @@ offset), then calls bsr_parallel_top_k_similarity_search on the whole query batc
   gtau_fallback  no merged list of the global-threshold search certifies (BSR_INJECT_FAULT):
              every query takes the collective fallback (the standard parallel search);
   no_gtau    the global threshold turned off (BSR_GLOBAL_TAU=0): the standard parallel search.
+  phase_a0   the last rank's global-threshold phase A fails before its header (BSR_INJECT_FAULT):
+             the header carries the failure, every rank takes the standard path;
+  phase_a1   the same after its header: the rank takes part in every collective, poisoned, and
+             every query takes the collective fallback.
   record     as normal, and every all-gather's receive buffer is recorded (Comm.host's record):
              the script a loopback communicator replays (tests/test_gpu_multirank.py).
   c3, c5     BASELINE configs at full size on the global-threshold path: configs[2]
@@ -79,6 +83,8 @@ def main():
         os.environ["BSR_INJECT_FAULT"] = f"header_hook:{a.world - 1}"
     if a.case == "gtau_fallback":
         os.environ["BSR_INJECT_FAULT"] = "gtau_uncertified"
+    if a.case in ("phase_a0", "phase_a1"):
+        os.environ["BSR_INJECT_FAULT"] = f"{a.case}:{a.world - 1}"
     if a.case == "no_gtau":
         os.environ["BSR_GLOBAL_TAU"] = "0"
     import torch  # noqa: F401  (before libbsr: one HIP runtime per process, tests/conftest.py)

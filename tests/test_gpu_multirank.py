@@ -126,6 +126,26 @@ def test_parallel_search_header_hook_fault(bsr_mod, oracle_mod, gpu, corpus, tmp
     _same(res[0], _want(oracle_mod, rows, q, 0, s_last))
 
 
+def test_parallel_search_phase_a_faults(bsr_mod, oracle_mod, gpu, corpus, tmp_path):
+    """a failing global-threshold phase A never leaves a peer blocked.  Before the
+    header (phase_a0) the failure rides in the header and every rank takes the standard path (the
+    failing rank contributes an empty list); after it (phase_a1) the rank stays in every collective
+    with a poisoned contribution, no merged list certifies, and the collective fallback -- where
+    the rank searches again -- gives the complete result."""
+    world = 3
+    rows, q = corpus
+    s_last = bsr_mod.interval_by_rank(world - 1, world, mr_worker.N).start_index
+    res = _run(world, "phase_a0", tmp_path)
+    assert int(res[world - 1]["status"]) == -3 and b"phase A, query prep" in res[world - 1]["msg"].tobytes()
+    assert int(res[1]["status"]) == 0 and int(res[0]["status"]) == 0
+    _same(res[0], _want(oracle_mod, rows, q, 0, s_last))
+    res = _run(world, "phase_a1", tmp_path)
+    assert int(res[world - 1]["status"]) == -3 and b"phase A, sample pass" in res[world - 1]["msg"].tobytes()
+    assert int(res[1]["status"]) == 0 and int(res[0]["status"]) == 0
+    assert int(res[0]["fallback"]) == len(q)
+    _same(res[0], _want(oracle_mod, rows, q))
+
+
 def test_parallel_search_failing_root(bsr_mod, oracle_mod, gpu, corpus, tmp_path):
     world = 2
     rows, q = corpus
@@ -272,5 +292,121 @@ def test_loopback_replays_recorded_run(bsr_mod, gpu, corpus, tmp_path):
     assert st == 0, bsr_mod.lib().bsr_last_error()
     _same({"idx": oi, "dist": od, "cnt": oc}, (res[0]["idx"], res[0]["dist"], res[0]["cnt"]))
     assert comm.loopback_stats() == (9, 0)
+    comm.close()
+    ix.close()
+
+
+# ---- real RCCL at P = 1: every collective of the parallel search ---------
+def _search_into_host_arrays(bsr_mod, comm, ix, q, k):
+    """The parallel search with the root's outputs in coherent pinned host memory (bsr_host_alloc):
+    the global-threshold merge writes its rows there directly (BSR_PATH_DIRECT_OUT)."""
+    oi = bsr_mod.host_array((len(q), k), np.uint64)
+    od = bsr_mod.host_array((len(q), k), np.float32)
+    oc = bsr_mod.host_array(len(q), np.uint32)
+    oi[:] = 7
+    od[:] = -1.0
+    oc[:] = 999
+    qq = np.ascontiguousarray(q, np.float32)
+    st = bsr_mod.lib().bsr_parallel_top_k_similarity_search(comm._h, ix._h, qq.ctypes.data, len(q), k,
+                                                            oi.ctypes.data, od.ctypes.data, oc.ctypes.data)
+    assert st == 0, bsr_mod.lib().bsr_last_error()
+    return {"idx": oi, "dist": od, "cnt": oc}
+
+
+def test_rccl_forced_collectives_single_rank(bsr_mod, oracle_mod, gpu, corpus, monkeypatch):
+    """BSR_FORCE_COLLECTIVES=1 makes a one-rank RCCL communicator take the multi-rank branch
+    (src/mpi_helpers/metrics.rs:174-206 with size 1), so every RCCL call the 8-GPU run makes runs
+    here on hardware: the header all-gather on the communicator's stream; the global threshold's
+    sample-key and result-buffer all-gathers on the index's stream, the merge, its certification
+    and publication (into the caller's pinned outputs directly, with the uncertified queries'
+    rows patched in); the collective fallback; and the standard path's group of three list
+    all-gathers with the device merge.  Every result bit-exact against the oracle."""
+    monkeypatch.setenv("BSR_FORCE_COLLECTIVES", "1")
+    P = bsr_mod
+    rows, q = corpus
+    want = _want(oracle_mod, rows, q)
+    ix = bsr_mod.Index(mr_worker.D, max_k=64, device=0)
+    ix.load(rows, 0)
+    comm = bsr_mod.Comm(bsr_mod.Comm.unique_id(), 0, 1, 0)
+    gt_bits = P.BSR_PATH_COLLECTIVE | P.BSR_PATH_GLOBAL_TAU
+    # 1. the global-threshold search, twice (buffers reused)
+    for rep in range(2):
+        got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
+        st = ix.last_stats()
+        assert st.parallel_path & gt_bits == gt_bits, (rep, st.parallel_path)
+        assert st.n_candidates == 0 and st.n_fallback == 0, (st.n_candidates, st.n_fallback)
+        _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
+    # 2. the root's outputs in coherent pinned memory: the merge writes them directly
+    r = _search_into_host_arrays(bsr_mod, comm, ix, q, mr_worker.K)
+    assert ix.last_stats().parallel_path == gt_bits | P.BSR_PATH_DIRECT_OUT, ix.last_stats().parallel_path
+    _same(r, want)
+    # 3. no merged list certifies: every query's rows come from the collective fallback (the
+    # standard path's RCCL group and device merge), patched into the direct outputs
+    monkeypatch.setenv("BSR_INJECT_FAULT", "gtau_uncertified")
+    r = _search_into_host_arrays(bsr_mod, comm, ix, q, mr_worker.K)
+    st = ix.last_stats()
+    assert st.parallel_path == gt_bits | P.BSR_PATH_DIRECT_OUT | P.BSR_PATH_FALLBACK, st.parallel_path
+    assert st.n_fallback == len(q)
+    _same(r, want)
+    # 4. phase A fails after the header (poisoned contribution): every query through the fallback,
+    # where this rank searches again -- the root's rows are complete
+    monkeypatch.setenv("BSR_INJECT_FAULT", "phase_a1")
+    got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
+    st = ix.last_stats()
+    assert st.parallel_path & P.BSR_PATH_FALLBACK and st.n_fallback == len(q), (st.parallel_path, st.n_fallback)
+    _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
+    monkeypatch.delenv("BSR_INJECT_FAULT")
+    # 5. the standard path: header from the search's hook, the group of three all-gathers, the
+    # device merge -- a 40-query batch with the global threshold off, and a 5-query batch (<= 16)
+    monkeypatch.setenv("BSR_GLOBAL_TAU", "0")
+    got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
+    assert ix.last_stats().parallel_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
+    _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
+    monkeypatch.delenv("BSR_GLOBAL_TAU")
+    small = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q[:5], mr_worker.K)
+    assert ix.last_stats().parallel_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
+    _same({"idx": small[0], "dist": small[1], "cnt": small[2]}, _want(oracle_mod, rows, q[:5]))
+    # 6. without the switch a one-rank communicator skips the collectives (the local lists)
+    monkeypatch.delenv("BSR_FORCE_COLLECTIVES")
+    got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
+    assert ix.last_stats().parallel_path == 0
+    _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
+    comm.close()
+    ix.close()
+
+
+def test_rccl_forced_collectives_configs2_shard(bsr_mod, oracle_mod, gpu, monkeypatch):
+    """The same at an 8-GPU run's operating point: rank 0's configs[2] shard (1.25M of the 10M
+    synthetic rows, 1000 queries on the device, k = 10) through a one-rank RCCL communicator with
+    the collectives forced -- the global-threshold path with every all-gather real RCCL; a subset
+    of queries (planted rows among them) bit-exact against the oracle over the shard."""
+    import torch
+    import test_gpu_full_size as fs
+    monkeypatch.setenv("BSR_FORCE_COLLECTIVES", "1")
+    n_total, nq, k = 10_000_000, 1000, 10
+    iv = bsr_mod.interval_by_rank(0, 8, n_total)
+    n = iv.get_count()
+    rows = torch.empty((n, mr_worker.D), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(rows.data_ptr(), 0, n, mr_worker.D, mr_worker.SEED)
+    torch.cuda.synchronize()
+    ix = bsr_mod.Index(mr_worker.D, max_k=k, device=0)
+    ix.load(rows, 0)
+    del rows
+    torch.cuda.empty_cache()
+    plant = [(0, 0), (1, n - 1), (2, 600_001)]
+    q = mr_worker.device_queries(bsr_mod, torch, nq, plant, False)
+    comm = bsr_mod.Comm(bsr_mod.Comm.unique_id(), 0, 1, 0)
+    for rep in range(2):
+        got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, k)
+        st = ix.last_stats()
+        bits = bsr_mod.BSR_PATH_COLLECTIVE | bsr_mod.BSR_PATH_GLOBAL_TAU
+        assert st.parallel_path & bits == bits, st.parallel_path
+        assert st.n_fallback <= nq // 200, st.n_fallback
+        fs._check_properties(got, n, k, "forced collectives, 1.25M shard")
+        for pos, row in plant:
+            assert got[0][pos, 0] == row and got[1][pos, 0] == 0.0, (pos, row, got[0][pos, :3])
+    sub = [0, 1, 2, 5, nq - 1]
+    want = fs._chunked_oracle(bsr_mod, oracle_mod, n, q[sub].cpu().numpy(), k)
+    fs._assert_same(got, want, sub, "forced collectives, 1.25M shard vs oracle")
     comm.close()
     ix.close()

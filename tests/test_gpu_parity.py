@@ -342,12 +342,14 @@ def test_published_rescue_and_fallback_rows(bsr_mod, oracle_mod, gpu, nq, n_resc
     n, dim, k = 60000, 768, 10
     rows = rng.uniform(-1, 1, (n, dim)).astype(np.float32)
     qs = rng.uniform(-1, 1, (nq, dim)).astype(np.float32)
-    perm = rng.permutation(n)
+    # The near-duplicates sit only at rows the sample pass never reads (row % 32 != 0, the
+    # every-32nd-row sample, csrc/index.cpp sample_pass): tau0 is then set by the uniform rows for
+    # any seed, the duplicates all pass it, and the rescue queries' first pass cannot certify -- the
+    # second chance runs by construction.
+    unsampled = np.flatnonzero(np.arange(n) % 32 != 0)
+    perm = unsampled[rng.permutation(len(unsampled))]
     at = 0
-    # (one query: 120 near-duplicates, so that fewer than ks = 8 of them fall into its every-32nd-row
-    # sample -- with 200, this seed samples enough of them to put tau0 among the duplicates, and the
-    # query legitimately takes the exact scan)
-    m_rescue = 200 if nq > 1 else 120
+    m_rescue = 200
     for q, m in [(q, m_rescue) for q in range(n_rescue)] + [(q, 1500) for q in range(n_rescue, n_rescue + n_over)]:
         pos = perm[at:at + m]
         at += m
