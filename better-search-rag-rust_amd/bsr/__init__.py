@@ -47,12 +47,14 @@ BSR_MAX_K = 256
 BSR_FLAG_EXACT_ONLY = 1
 BSR_FLAG_PROFILE = 2
 BSR_FLAG_FILTER_BF16 = 4   # retired (round 4): bsr_index_create returns BSR_E_INVALID
-# SearchStats.parallel_path bits (include/bsr.h)
+# SearchStats.search_path bits (include/bsr.h)
 BSR_PATH_COLLECTIVE = 1
 BSR_PATH_GLOBAL_TAU = 2
 BSR_PATH_DIRECT_OUT = 4
 BSR_PATH_DEVICE_MERGE = 8
 BSR_PATH_FALLBACK = 16
+BSR_PATH_SKINNY_TOP = 32
+BSR_PATH_TOP_RERUN = 64
 FILTER_I8 = 0
 ROOT = 0  # src/mpi_helpers/mod.rs:8
 
@@ -77,7 +79,7 @@ class SearchStats(ctypes.Structure):
                 ("n_fallback", ctypes.c_uint32), ("n_candidates", ctypes.c_uint32),
                 ("n_emitted", ctypes.c_uint64), ("filter_op", ctypes.c_uint32),
                 ("row_ebound", ctypes.c_float), ("n_rescued", ctypes.c_uint32),
-                ("graph_replay", ctypes.c_uint32), ("parallel_path", ctypes.c_uint32)]
+                ("graph_replay", ctypes.c_uint32), ("search_path", ctypes.c_uint32)]
 
 
 class Profile(ctypes.Structure):

@@ -986,7 +986,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // 4. the uncertified queries, collectively (every rank holds the same F)
     const uint32_t nf = hw[0];
     ix->stats.n_fallback = nf;
-    ix->stats.parallel_path = path;
+    ix->stats.search_path = path;
     uint32_t* m_cnt = direct ? out_count : reinterpret_cast<uint32_t*>(hm + o_cnt);
     float* m_dist = direct ? out_dist : reinterpret_cast<float*>(hm + o_dist);
     uint64_t* m_idx = direct ? out_idx : reinterpret_cast<uint64_t*>(hm + o_idx);
@@ -1021,7 +1021,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
         ix->stats.n_candidates = 0;  // (this search's path: every emitted row rescored)
         ix->stats.n_fallback = nf;
         ix->stats.n_queries = nq;
-        ix->stats.parallel_path = path | BSR_PATH_FALLBACK;
+        ix->stats.search_path = path | BSR_PATH_FALLBACK;
         if (poisoned && !root) return set_error(a_err, "%s", a_msg.c_str());
         if (staged != BSR_OK && !root) return set_error(staged, "%s", staged_err.c_str());
         // (the root's staging failed: its fallback search had no queries; report the real cause)
@@ -1229,7 +1229,7 @@ static int parallel_impl(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     // succeeded, i.e. that buffer is sized for this batch; host transport: the root's lists
     // come up to its GPU for the same merge)
     const bool dev_merge = ok && device_merge_fits((uint32_t)c->size, k, k);
-    if (ix) ix->stats.parallel_path = BSR_PATH_COLLECTIVE | (root && dev_merge ? BSR_PATH_DEVICE_MERGE : 0u);
+    if (ix) ix->stats.search_path |= BSR_PATH_COLLECTIVE | (root && dev_merge ? BSR_PATH_DEVICE_MERGE : 0u);
     hipStream_t xs = c->host_fn ? nullptr : (ok ? ix->stream : c->stream);
     BSR_TRY(exchange_lists(c, li, ld, lc, !ok, nq, k, xs, !dev_merge || c->host_fn));
     if (ok) bsr_index_collect_profile_impl(ix);

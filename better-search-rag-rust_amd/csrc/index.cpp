@@ -407,13 +407,28 @@ static int sample_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, ui
 static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k);
 
 
+// The self-thresholded single-query path (round 6, DESIGN.md §5 tiny batches): batches of <= 16
+// queries over shards of >= kSkinnyTopMinRows rows, k' <= 63, rows of <= 16 K slices, with the
+// tiny-batch rescore kernel (BSR_SKINNY_TOP=0 turns it off, for A/B runs).  No sample pass and
+// no tau0: the skinny filter keeps every wave's 4 best keys per query, the rescore selects the k'
+// best of them.  Returns the lists' slots per query (0: the thresholded path).
+static uint32_t top_slots(const bsr_index* ix, uint32_t nq, uint32_t k) {
+    const char* v = getenv("BSR_SKINNY_TOP");
+    if ((v && v[0] == '0') || ix->force_threshold) return 0;
+    if (nq > kSkinnyMaxQ || ix->n < kSkinnyTopMinRows || kp_for(k) > 63 || k > 64 || ix->op_row_bytes > 16 * 64 ||
+        ix->ld % 64 != 0 || ix->ld > 1024 || !rescore_kp_enabled())
+        return 0;
+    const uint32_t slots = 4 * skinny_top_waves((uint32_t)ix->n);
+    return slots <= 16u * ix->ld ? slots : 0;  // (k_rescore_kp holds 16 keys per lane)
+}
+
 // Buffers of the candidate stage for a batch (k' = kp_for(k) candidates, lists of cap keys).
 static int filter_buffers(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     // k' candidates, (k'+1) % 64 == 0, about 3k: the k-th exact score must clear the (k'+1)-th
     // approximate one by E_q, and in a Gaussian-like tail that takes ~3x as many rows at
     // E_q/sigma ~ 0.26.  63 for k <= 10, 191 for k = 50, 383 for k = 100.
     const uint32_t kp = kp_for(k);
-    const uint32_t cap = cap_for(k);
+    const uint32_t cap = std::max(cap_for(k), top_slots(ix, nq, k));
     ix->stats.n_candidates = kp;
     BSR_TRY(ix->tau.ensure((size_t)qpad * sizeof(float)));
     BSR_TRY(ix->cand.ensure((size_t)qpad * cap * sizeof(uint64_t)));
@@ -503,15 +518,39 @@ static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     return BSR_OK;
 }
 
+// The self-thresholded filter pass: every wave's 4 best keys per query (launch_filter_skinny_top).
+static int top_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
+    BSR_TRY(filter_buffers(ix, nq, qpad, k));
+    GemmArgs g = gemm_args(ix, qpad);
+    g.a_stride = ix->op_row_bytes;
+    g.a_scale_rows = kQuantBlock;
+    g.n_rows = (uint32_t)ix->n;
+    g.n_rt = (uint32_t)((ix->n + kFilterTile - 1) / kFilterTile);
+    g.cand = ix->cand.as<uint64_t>();
+    g.cnt = ix->cnt.as<uint32_t>();
+    g.cap = top_slots(ix, nq, k);
+    g.status = ix->d_status;
+    BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
+        return launch_filter_skinny_top(g, ix->stream, e0, e1);
+    }));
+    return BSR_OK;
+}
+
 // Candidate stage (steps 2-5) for every query of the batch.
 static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uint32_t* next_status, bool publish) {
-    BSR_TRY(sample_pass(ix, nq, qpad, k, nullptr));
-    BSR_TRY(emit_pass(ix, nq, qpad, k));
+    const uint32_t top = top_slots(ix, nq, k);
+    if (top) {
+        BSR_TRY(top_pass(ix, nq, qpad, k));
+    } else {
+        BSR_TRY(sample_pass(ix, nq, qpad, k, nullptr));
+        BSR_TRY(emit_pass(ix, nq, qpad, k));
+    }
     const uint32_t kp = kp_for(k);
-    const uint32_t cap = cap_for(k);
+    const uint32_t cap = top ? top : cap_for(k);
     uint32_t* status = ix->d_status;
-    // lists of <= 1024 keys (k <= 10): the rescore kernel selects its own k' candidates
-    const bool fused_select = cap <= kFusedSelectCap;
+    // lists of <= 1024 keys (k <= 10): the rescore kernel selects its own k' candidates (the
+    // self-thresholded path: always, every wave of the tiny-batch kernel taking part)
+    const bool fused_select = top || cap <= kFusedSelectCap;
     if (!fused_select) {
         ev_begin(ix, ix->ev_select);
         BSR_HIP(launch_select_cand(ix->cand.as<uint64_t>(), ix->cnt.as<uint32_t>(), cap, nq, ix->tau.as<float>(),
@@ -555,6 +594,12 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
         ra.cap = cap;
         ra.tau0 = ix->tau.as<float>();
     }
+    if (top) {
+        ra.top_w = top / 4;
+        ra.qflags = ix->qflags.as<uint32_t>();
+        ra.top_tau = ix->tau.as<float>();  // (the second chance's tau0)
+        ra.top_cnt = ix->cnt.as<uint32_t>();
+    }
     BSR_HIP(launch_rescore(ra, ix->stream));
     // Second chance, in the same stream (and graph): a query that failed certification is
     // rescored over EVERY row it emitted (~4k'), certified against tau0 -- far less than a
@@ -562,6 +607,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     // too goes to fail2 (exact scan, host-driven).
     RescoreArgs rb = ra;
     rb.sel = 0;
+    rb.top_w = 0;
     rb.n_items = nq;
     rb.n_items_dev = status + kStFail;
     rb.qlist = ix->fail.as<uint32_t>();
@@ -722,13 +768,15 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
 
     // Every filtered batch is graph-capturable; a timed search (profile level >= 1) launches
     // directly, its events recorded on the stream (launch_timed).
-    const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0);
+    const bool top = use_filter && top_slots(ix, nq, k) != 0;
+    if (top) stats.search_path |= BSR_PATH_SKINNY_TOP;
+    const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0) && !force_threshold;
     SearchGraph& gs = graphs[cur];
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
-                            warm.timed == (profiling(ix) ? prof_level : 0);
+                            warm.timed == (profiling(ix) ? prof_level : 0) && warm.top == top;
     const int timed_level = profiling(ix) ? prof_level : 0;
     if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen &&
-        gs.timed == timed_level) {
+        gs.timed == timed_level && gs.top == top) {
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         stats.n_candidates = kp_for(k);
         ++graph_replays;
@@ -752,13 +800,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(BSR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level};
+        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level, top};
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         ++graph_replays;
         stats.graph_replay = 1;
     } else {
         BSR_TRY(enqueue_search());
-        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level};
+        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, top};
     }
     next_status_clean = true;
     int hook_st = BSR_OK;
@@ -806,6 +854,18 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
             BSR_HIP(hipMemcpyAsync(h_qflags.data(), qflags.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    stream));
             BSR_HIP(hipStreamSynchronize(stream));
+            bool served_failed = false;
+            for (uint32_t q : h_fail) served_failed |= !(h_qflags[q] & kQueryNoApprox);
+            if (top && served_failed) {
+                // The self-thresholded path left a query it serves uncertified (more than a wave's 4
+                // best of its rows lie near the top: a cluster of near-duplicates): the batch again
+                // on the thresholded path, directly launched, whose own failures take the exact scan.
+                force_threshold = true;
+                const int r = search_device(queries, nq, k);
+                force_threshold = false;
+                stats.search_path |= BSR_PATH_SKINNY_TOP | BSR_PATH_TOP_RERUN;
+                return r;
+            }
             std::sort(h_fail.begin(), h_fail.end());
             for (uint32_t q : h_fail) {
                 exact_ids.push_back((int32_t)q);

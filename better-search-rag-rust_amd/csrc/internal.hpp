@@ -124,7 +124,11 @@ struct bsr_index {
         const float* qsrc = nullptr;
         uint64_t n = 0, gen = 0;
         int timed = 0;  // profile level it was captured at (always 0: timed searches launch directly)
+        bool top = false;  // the self-thresholded single-query path (round 6)
     };
+    // (round 6) the batch is searched again on the thresholded path: the self-thresholded path
+    // left a query uncertified (direct launches, no graph)
+    bool force_threshold = false;
     bool capturing = false;    // a search is being captured into a graph
     SearchGraph graphs[2];
     SearchGraph warm;  // the last direct search of a graphable shape (no exec)

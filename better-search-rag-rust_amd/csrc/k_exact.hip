@@ -403,8 +403,10 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
             const uint32_t nchk = NC ? NC : nch;
             for (uint32_t base = QPW > 1 ? 0u : 64u * w; base < c; base += 64 * W) {
                 const uint32_t ci = base + lane, cc = ci < c ? ci : 0;
+                const uint64_t ck = all ? a.cand_keys[(uint64_t)q * a.cap + cc] : 0ull;
+                const bool valid = ci < c && ck != kKeyNone;  // (an empty slot of a list: no row)
                 const uint32_t myrow = sel ? sel_row
-                                     : all ? key_row(a.cand_keys[(uint64_t)q * a.cap + cc])
+                                     : all ? (ck != kKeyNone ? key_row(ck) : 0u)
                                            : a.cand_rows[(uint64_t)q * a.kp + cc];
                 float acc[1] = {-0.0f}, mx[1] = {0.0f};
                 uint32_t lrow[16];
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
                     }
                 }
                 const float d = finish_distance(acc[0], mx[0], a.na[myrow], mag_b);
-                L.offer(ci < c ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
+                L.offer(valid ? dist_key(d, myrow) : kKeyNone, (int)a.k, thr);
             }
         };
         if (qlds && nch == 12) scan(std::true_type{}, std::integral_constant<uint32_t, 12>{});
@@ -667,6 +669,138 @@ __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
 // arithmetic and its order are k_rescore's, so the distances are its bits; wave 0 finishes
 // (top-k, certification, result rows) as k_rescore mode S does.  One-wave k_rescore spent ~30 us
 // on one query's 63 rows: 12 chunks, each behind its own load latency.
+// The self-thresholded path's selection (RescoreArgs::top_w), every wave of the workgroup: the
+// query's 4 * top_w keys (ascending 4-lists, one per wave of the skinny filter) in registers,
+// JU per lane; the bound X of the rows outside the lists (the smallest 4th key: every row a wave
+// left out scores at most its 4th); a block-wide radix select of the (kp+1)-th smallest key T
+// (high words first, then -- only when several keys share T's high word -- the low words), the
+// kp keys below it compacted into lsel.  tau_x = max(score(T), score(X)): every row outside the
+// candidates scores at most that.  The keys below X are then compacted to the front of the
+// query's list for the second chance (certified against score(X)).
+template <int JU>
+__device__ __forceinline__ void top_select_t(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c,
+                                             float& s_tx, uint32_t& s_ov, int w, int nw, int lane) {
+    __shared__ uint32_t s_cnt[2][16];
+    __shared__ uint64_t s_x[16];
+    __shared__ uint32_t s_pos, s_pos2, s_tl;
+    const uint32_t U = 4 * a.top_w, stride = (uint32_t)nw * 64;
+    const bool served = !(a.qflags[q] & kQueryNoApprox);
+    uint64_t* const list = const_cast<uint64_t*>(a.cand_keys) + (uint64_t)q * a.cap;
+    uint64_t x[JU];
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+        const uint32_t i = j * stride + (uint32_t)w * 64 + lane;
+        x[j] = (served && i < U) ? list[i] : kKeyNone;
+    }
+    if (threadIdx.x == 0) { s_pos = 0; s_pos2 = 0; }
+    int par = 0;
+    // block-wide count of the keys satisfying pred (one barrier)
+    auto count = [&](auto pred) -> uint32_t {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < JU; ++j) c += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && pred(x[j])));
+        if (lane == 0) s_cnt[par][w] = c;
+        __syncthreads();
+        uint32_t t = 0;
+        for (int v = 0; v < nw; ++v) t += s_cnt[par][v];
+        par ^= 1;
+        return t;
+    };
+    // X: the smallest of the lists' 4th keys (list slot 3: lanes with lane % 4 == 3, as 64 nw is
+    // a multiple of 4); the high-word range of the valid keys
+    uint64_t mx = kKeyNone;
+    uint32_t hmin = ~0u, hmax = 0;
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+        if ((lane & 3) == 3) mx = x[j] < mx ? x[j] : mx;
+        if (x[j] != kKeyNone) {
+            hmin = min(hmin, (uint32_t)(x[j] >> 32));
+            hmax = max(hmax, (uint32_t)(x[j] >> 32));
+        }
+    }
+    {
+        uint32_t lo = (uint32_t)mx, hi = (uint32_t)(mx >> 32);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t lo2 = (uint32_t)__shfl_xor((int)lo, off, kWave), hi2 = (uint32_t)__shfl_xor((int)hi, off, kWave);
+            const bool lt = hi2 < hi || (hi2 == hi && lo2 < lo);
+            lo = lt ? lo2 : lo;
+            hi = lt ? hi2 : hi;
+        }
+        mx = ((uint64_t)hi << 32) | lo;
+    }
+    hmin = wave_reduce_u32(hmin, [](uint32_t u, uint32_t v) { return min(u, v); });
+    hmax = wave_reduce_u32(hmax, [](uint32_t u, uint32_t v) { return max(u, v); });
+    if (lane == 0) {
+        s_x[w] = mx;
+        s_cnt[0][w] = hmin;
+        s_cnt[1][w] = hmax;
+    }
+    __syncthreads();
+    uint64_t X = kKeyNone;
+    hmin = ~0u;
+    hmax = 0;
+    for (int v = 0; v < nw; ++v) {
+        X = s_x[v] < X ? s_x[v] : X;
+        hmin = min(hmin, s_cnt[0][v]);
+        hmax = max(hmax, s_cnt[1][v]);
+    }
+    __syncthreads();  // (s_cnt is the count buffer from here)
+    const float tx_trunc = X == kKeyNone ? -INFINITY : score_key_score(X);
+    const uint32_t K = a.kp + 1;
+    const uint32_t V = count([](uint64_t) { return true; });
+    uint64_t T = kKeyNone;
+    float tx = tx_trunc;
+    if (V > a.kp) {
+        const uint32_t diff = hmin ^ hmax;
+        const int top = diff ? 31 - __builtin_clz(diff) : -1;
+        uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
+        for (int b = top; b >= 0; --b) {
+            const uint32_t t = Th | (1u << b);
+            if (count([t](uint64_t k) { return (uint32_t)(k >> 32) < t; }) < K) Th = t;
+        }
+        const uint32_t lt = count([Th](uint64_t k) { return (uint32_t)(k >> 32) < Th; });
+        const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
+        const uint32_t eq = count([Th](uint64_t k) { return (uint32_t)(k >> 32) == Th; });
+        uint32_t Tl = 0;
+        if (eq > 1) {
+            for (int b = 31; b >= 0; --b) {
+                const uint32_t t = Tl | (1u << b);
+                if (count([Th, t](uint64_t k) { return (uint32_t)(k >> 32) == Th && (uint32_t)k < t; }) < K2) Tl = t;
+            }
+        } else {  // the one key with high word Th (keys are unique: the row is the low word)
+#pragma unroll
+            for (int j = 0; j < JU; ++j)
+                if (x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th) s_tl = (uint32_t)x[j];
+            __syncthreads();
+            Tl = s_tl;
+        }
+        T = ((uint64_t)Th << 32) | Tl;
+        tx = fmaxf(score_key_score(T), tx_trunc);
+    }
+    // the candidates: every valid key below T (all of them when V <= kp), compacted into lsel
+#pragma unroll
+    for (int j = 0; j < JU; ++j)
+        if (x[j] != kKeyNone && x[j] < T) lsel[atomicAdd(&s_pos, 1u)] = key_row(x[j]);
+    __syncthreads();  // (every key was read from the list above: it may be rewritten now)
+    // the second chance's input: the keys below X at the front of the list, their count
+#pragma unroll
+    for (int j = 0; j < JU; ++j)
+        if (x[j] != kKeyNone && x[j] < X) list[atomicAdd(&s_pos2, 1u)] = x[j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_c = s_pos;
+        s_tx = served ? tx : INFINITY;
+        s_ov = served ? 0u : 1u;
+        a.top_cnt[q] = s_pos2;
+        a.top_tau[q] = served ? tx_trunc : INFINITY;
+    }
+}
+__device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c, float& s_tx,
+                                           uint32_t& s_ov, int w, int nw, int lane) {
+    top_select_t<16>(a, q, lsel, s_c, s_tx, s_ov, w, nw, lane);
+}
+
 // ------------------------------------------------------------------------------------
 constexpr int kKpStage = 64 * 68;  // 64 rows x one chunk (stride 68)
 template <int E>
@@ -685,7 +819,9 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     const uint32_t ld = a.ld, dim = a.dim;
     // the query's chunk of this wave, staged in LDS (read as broadcasts)
     if ((uint32_t)(w * 64 + lane) < ld) ldq[w * 64 + lane] = a.qf32[(uint64_t)q * ld + w * 64 + lane];
-    if (w == 0) {
+    if (a.top_w) {
+        top_select(a, q, lsel, s_c, s_tx, s_ov, w, nw, lane);
+    } else if (w == 0) {
         constexpr int NR = 16;
         uint64_t xk[NR];
         const uint64_t* src = a.cand_keys + (uint64_t)q * a.cap;
@@ -1249,6 +1385,11 @@ extern "C" int bsr_lab_rescore_stamps(uint64_t* out, int n) {
 #ifndef BSR_GT_RESCORE_P
 #define BSR_GT_RESCORE_P 2
 #endif
+bool rescore_kp_enabled() {
+    const char* v = getenv("BSR_RESCORE_KP");
+    return !(v && v[0] == '0');
+}
+
 hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     if (!a_in.n_items) return hipSuccess;
     RescoreArgs a = a_in;
@@ -1256,12 +1397,12 @@ hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     const uint32_t e = (a.k + 63) / 64;
     // the first pass (mode S) of a tiny batch: one workgroup per query, one wave per chunk
     // (BSR_RESCORE_KP=0: the one-wave kernel instead, for A/B runs)
-    static const bool kp_on = [] {
-        const char* v = getenv("BSR_RESCORE_KP");
-        return !(v && v[0] == '0');
-    }();
+    static const bool kp_on = rescore_kp_enabled();
+    if (a.top_w && !(kp_on && a.n_items <= 16 && a.ld % 64 == 0 && a.ld <= 1024 && a.k <= 64 && a.kp <= 63 &&
+                     4 * a.top_w <= 16u * (a.ld / 64) * 64))
+        return hipErrorInvalidValue;  // (the self-thresholded path needs k_rescore_kp: the caller checks)
     if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && a.n_items <= 16 && a.ld % 64 == 0 &&
-        a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && a.cap <= 1024) {
+        a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && (a.cap <= 1024 || a.top_w)) {
         hipLaunchKernelGGL(k_rescore_kp<1>, dim3(a.n_items), dim3(a.ld), 0, s, a);
         return hipGetLastError();
     }

@@ -536,7 +536,12 @@ extern "C" int bsr_lab_filter_stamps(unsigned long long* out, int reset) {
 // query tile (round 3); 1 or 2 = half or all of the tiles dynamic (no gain: r04c_fab_*.txt).
 // L2, FW (lab, round 5): level 2's passing row blocks as a bool array (1) instead of a bit mask
 // (0); FW = 0: no explicit vmcnt(0) in the flush path.
-template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0, int L2 = 0, int FW = 1>
+// KSB (lab, round 6, timing only at tau = inf): a bound on the K-split wave pair (each wave of a
+// pair holding 64 queries for half of K, the partial sums exchanged through LDS): 1 = every other
+// fragment read skipped (the pair's halved LDS fragment bytes per MFMA); 2 = that plus the
+// exchange's cost per wave and tile (16 KiB of accumulators written to LDS, read back and added).
+template <bool EMIT, int NK, int EPI = 0, int TAILX = 8, int GANG = 2, int RING = 0, int L2 = 0, int FW = 1,
+          int KSB = 0>
 __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
     constexpr bool DEFER = EPI == 1, STAGE = EPI == 2 && EMIT;
     // EPI = 3 (lab, stagger): only waves 4-7 -- the SIMD partners of waves 0-3 -- defer their
@@ -919,8 +924,13 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (rb < 4) read_frag(jj, rb + 4);
-                else read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
+                if (KSB && (rb & 1)) {
+                    // (lab KSB: this fragment read skipped; the register keeps an older fragment)
+                } else if (rb < 4) {
+                    read_frag(jj, rb + 4);
+                } else {
+                    read_frag(jj + 1, rb - 4);  // (past the stream's end: unused)
+                }
                 // (the atomic completed at the kt = 3 barrier; the LDS write completes, in order,
                 // before wave 0's next fragment reads are waited for -- well before kt = 5's barrier)
                 if (kt == kClaimUse && rb == 0 && req && tid == 0) lds_ids[t & 1] = tail_id(claimed);
@@ -968,6 +978,16 @@ __global__ __launch_bounds__(512, 1) void k_filter_qs16(GemmArgs p) {
                 __builtin_amdgcn_sched_barrier(0);
             }
         });
+        if constexpr (KSB == 2 && EMIT) {
+            // (lab KSB = 2, timing only) the pair's exchange: 16 KiB of this wave's accumulators to
+            // LDS (the emission rings' space: unused at tau = inf), read back and added
+            i32x4v_t* xs = reinterpret_cast<i32x4v_t*>(lds + S * SLOT + (w % 5) * 16384) + lane;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) xs[i * 64] = acc[i >> 1][i & 1];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i >> 1][i & 1] += xs[(15 - i) * 64];
+        }
         // ---- epilogue: block (rb, nb) holds rows 16rb + 4(lane >> 4) + r, query qq[nb]
         const float sc[4] = {scv.x, scv.y, scv.z, scv.w};
         bool stored = false;
@@ -1315,12 +1335,28 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
 // MFMAs and epilogue run.  EMIT: units dealt round-robin over all waves (small tail).
 // SAMPLE: a wave takes the two units of one 32-sampled-row block back to back, so the
 // compact maximum over 32 sampled rows stays in a register.
+// TOP (round 6, the self-thresholded single-query path): units dealt as EMIT, no threshold;
+// each lane keeps the 4 best (score, row) keys of its rows, the four lanes of a query merge
+// them at the end, and the wave writes its 4 best keys per query to cand[q][wave][4] -- every
+// row of the wave not among them scores at most its 4th (tiny batches).
 // ------------------------------------------------------------------------------------
 #ifndef BSR_SKINNY_NT
 #define BSR_SKINNY_NT 0
 #endif
-template <bool EMIT, int NK>
+constexpr int kSkSample = 0, kSkEmit = 1, kSkTop = 2;
+// insert key x into the ascending 4-list t (smaller key = better score), keeping the best 4
+__device__ __forceinline__ void top4_insert(uint64_t (&t)[4], uint64_t x) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool lt = x < t[j];
+        const uint64_t lo = lt ? x : t[j];
+        x = lt ? t[j] : x;
+        t[j] = lo;
+    }
+}
+template <int MODE, int NK>
 __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
+    constexpr bool EMIT = MODE == kSkEmit, TOP = MODE == kSkTop, ROWS = EMIT || TOP;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t q = lane & 15, h = lane >> 4;
     const uint32_t nk = p.row_bytes / kSliceB;
@@ -1333,12 +1369,25 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     for (int s = 0; s < NK; ++s)
         fb[s] = s < (int)nk ? *reinterpret_cast<const i32x4_t*>(p.B + (uint64_t)q * p.row_bytes + h * 16 + s * kSliceB)
                             : i32x4_t{0, 0, 0, 0};
-    // unit sequence of this wave: EMIT u = wid + i*nwaves; SAMPLE u = 2(wid + j*nwaves) + (i&1)
+    // unit sequence of this wave: EMIT / TOP u = wid + i*nwaves; SAMPLE u = 2(wid + j*nwaves) + (i&1)
     auto unit_of = [&](uint32_t i) -> uint32_t {
-        return EMIT ? wid + i * nwaves : 2 * (wid + (i >> 1) * nwaves) + (i & 1);
+        return ROWS ? wid + i * nwaves : 2 * (wid + (i >> 1) * nwaves) + (i & 1);
     };
+    // TOP: the lane's 4 best keys (ascending) and the score of the 4th (-inf until it has 4)
+    uint64_t tk[4] = {kKeyNone, kKeyNone, kKeyNone, kKeyNone};
+    float tk3 = -INFINITY;
+    if (TOP && blockIdx.x == 0 && threadIdx.x < 16) {
+        // (the bookkeeping k_select_tau does on the thresholded path: every query's list is
+        // its 4 * nwaves slots, the status words of the rescores that follow start at 0)
+        p.cnt[threadIdx.x] = 4 * nwaves;
+        if (threadIdx.x == 0) { p.status[kStFail] = 0; p.status[kStEmitted] = 0; p.status[kStFail2] = 0; }
+    }
+    // TOP: unit u holds the strided rows u, u + n_units, ..., u + 15 n_units (A-row m = row
+    // m n_units + u), so a run of consecutive similar rows is spread over consecutive units, i.e.
+    // over different waves: no wave's 4 best are all from one cluster unless it spans > 2048 rows
+    auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t { return TOP ? m * n_units + u : u * 16 + m; };
     auto load = [&](i32x4_t (&fa)[NK], uint32_t u) {
-        uint32_t r = u * 16 + q;
+        uint32_t r = row_of(u, q);
         r = r < p.n_rows ? r : p.n_rows - 1;  // tail rows: clamped, never emitted
         const uint8_t* a = p.A + (uint64_t)r * p.a_stride + h * 16;
 #pragma unroll
@@ -1357,7 +1406,23 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
         for (int s = 0; s < NK; ++s)
             if (s < (int)nk) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
         // register i: tile row u*16 + 4h + i, query q
-        if constexpr (EMIT) {
+        if constexpr (TOP) {
+            float v[4];
+            uint32_t rw[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                rw[i] = row_of(u, 4 * h + i);
+                const float sc = p.a_scale[(rw[i] < p.n_rows ? rw[i] : p.n_rows - 1) / kQuantBlock];
+                v[i] = ((float)acc[i] * sc) * sbq;
+            }
+            const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+            if (mx >= tk3) {  // (rare once the lane holds 4 keys: ~4 ln(rows / 4) insertions)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (rw[i] < p.n_rows) top4_insert(tk, score_key(v[i], rw[i]));
+                tk3 = tk[3] == kKeyNone ? -INFINITY : score_key_score(tk[3]);
+            }
+        } else if constexpr (EMIT) {
             const float sc = p.a_scale[(u * 16) / kQuantBlock];
             float v[4];
 #pragma unroll
@@ -1397,21 +1462,43 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     };
     // this wave's unit count
     uint32_t n_my;
-    if (EMIT) {
+    if (ROWS) {
         n_my = wid < n_units ? (n_units - 1 - wid) / nwaves + 1 : 0;
     } else {
         const uint32_t n_blk = (n_units + 1) / 2;
         n_my = wid < n_blk ? 2 * ((n_blk - 1 - wid) / nwaves + 1) : 0;
     }
-    if (!n_my) return;
-    i32x4_t fa0[NK], fa1[NK];
-    load(fa0, unit_of(0));
-    for (uint32_t i = 0; i < n_my; i += 2) {
-        if (i + 1 < n_my) load(fa1, unit_of(i + 1));
-        process(fa0, unit_of(i));
-        if (i + 1 >= n_my) break;
-        if (i + 2 < n_my) load(fa0, unit_of(i + 2));
-        process(fa1, unit_of(i + 1));
+    if (n_my) {
+        i32x4_t fa0[NK], fa1[NK];
+        load(fa0, unit_of(0));
+        for (uint32_t i = 0; i < n_my; i += 2) {
+            if (i + 1 < n_my) load(fa1, unit_of(i + 1));
+            process(fa0, unit_of(i));
+            if (i + 1 >= n_my) break;
+            if (i + 2 < n_my) load(fa0, unit_of(i + 2));
+            process(fa1, unit_of(i + 1));
+        }
+    }
+    if constexpr (TOP) {
+        // the query's four lanes (h = 0..3: lanes q, q + 16, q + 32, q + 48) merge their lists:
+        // partners 16 apart, then 32 -- every lane then holds the wave's 4 best keys of query q
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            uint64_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)tk[j], off, kWave);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(tk[j] >> 32), off, kWave);
+                o[j] = ((uint64_t)hi << 32) | lo;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) top4_insert(tk, o[j]);
+        }
+        if (h == 0) {
+            uint64_t* dst = p.cand + ((uint64_t)q * nwaves + wid) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dst[j] = tk[j];
+        }
     }
 }
 
@@ -1735,24 +1822,33 @@ static uint32_t skinny_grid(uint32_t n_rows) {
     return wgs < 768 ? (wgs ? wgs : 1) : 768;  // 3 workgroups per CU (VGPR-limited occupancy)
 }
 // v2 for rows of <= 16 K steps (1024 int8), v1 beyond.
-template <bool EMIT>
+// v2's grid: 4 waves per workgroup, at most 512 workgroups (~170 VGPRs: 2 waves per SIMD)
+static uint32_t skinny2_grid(uint32_t n_rows) {
+    const uint32_t units = (n_rows + 15) / 16;
+    return std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
+}
+uint32_t skinny_top_waves(uint32_t n_rows) { return 4 * skinny2_grid(n_rows); }
+template <int MODE>
 static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB;
-    // v2 holds ~170 VGPRs: 2 waves per SIMD = 2 workgroups per CU
-    const uint32_t units = (a.n_rows + 15) / 16, g2 = std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
-    const dim3 g(nk <= 16 ? g2 : skinny_grid(a.n_rows)), b(256);
-    if (nk <= 4) BSR_KLAUNCH((k_filter_skinny2<EMIT, 4>), g, b, s, e0, e1, a);
-    else if (nk <= 8) BSR_KLAUNCH((k_filter_skinny2<EMIT, 8>), g, b, s, e0, e1, a);
-    else if (nk <= 12) BSR_KLAUNCH((k_filter_skinny2<EMIT, 12>), g, b, s, e0, e1, a);
-    else if (nk <= 16) BSR_KLAUNCH((k_filter_skinny2<EMIT, 16>), g, b, s, e0, e1, a);
-    else BSR_KLAUNCH(k_filter_skinny<EMIT>, g, b, s, e0, e1, a);
+    const dim3 g(nk <= 16 ? skinny2_grid(a.n_rows) : skinny_grid(a.n_rows)), b(256);
+    if (nk <= 4) BSR_KLAUNCH((k_filter_skinny2<MODE, 4>), g, b, s, e0, e1, a);
+    else if (nk <= 8) BSR_KLAUNCH((k_filter_skinny2<MODE, 8>), g, b, s, e0, e1, a);
+    else if (nk <= 12) BSR_KLAUNCH((k_filter_skinny2<MODE, 12>), g, b, s, e0, e1, a);
+    else if (nk <= 16) BSR_KLAUNCH((k_filter_skinny2<MODE, 16>), g, b, s, e0, e1, a);
+    else if constexpr (MODE != kSkTop) BSR_KLAUNCH(k_filter_skinny<MODE == kSkEmit>, g, b, s, e0, e1, a);
 }
 hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_skinny<false>(a, s, e0, e1);
+    launch_skinny<kSkSample>(a, s, e0, e1);
     return hipGetLastError();
 }
 hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    launch_skinny<true>(a, s, e0, e1);
+    launch_skinny<kSkEmit>(a, s, e0, e1);
+    return hipGetLastError();
+}
+hipError_t launch_filter_skinny_top(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (a.row_bytes / kSliceB > 16) return hipErrorInvalidValue;  // (v2 widths only: the caller checks)
+    launch_skinny<kSkTop>(a, s, e0, e1);
     return hipGetLastError();
 }
 

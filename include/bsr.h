@@ -104,15 +104,18 @@ typedef struct {
     uint32_t n_rescued;        /* queries certified by the second chance (all emitted rows) */
     uint32_t graph_replay;     /* 1: the search replayed a captured hipGraph (every filtered batch
                                   from the second search of its shape on, at profile level 0) */
-    uint32_t parallel_path;    /* bsr_parallel_top_k_similarity_search only: BSR_PATH_* bits */
+    uint32_t search_path;      /* BSR_PATH_* bits: which branches the last search took */
 } bsr_search_stats;
 
-/* bsr_search_stats.parallel_path: which branches the last parallel search took */
+/* bsr_search_stats.search_path: which branches the last search took (bits 1-16: the parallel
+ * search; 32, 64: a batch of <= 16 queries on the self-thresholded path) */
 #define BSR_PATH_COLLECTIVE 1u   /* the collectives ran (size > 1, or BSR_FORCE_COLLECTIVES=1) */
 #define BSR_PATH_GLOBAL_TAU 2u   /* the global-threshold search */
 #define BSR_PATH_DIRECT_OUT 4u   /* root: merged rows written straight into coherent pinned outputs */
 #define BSR_PATH_DEVICE_MERGE 8u /* root of the standard path: the device merge (k_merge_lists) */
 #define BSR_PATH_FALLBACK 16u    /* global threshold: uncertified queries took the collective fallback */
+#define BSR_PATH_SKINNY_TOP 32u  /* no sample pass: every filter wave's 4 best keys per query */
+#define BSR_PATH_TOP_RERUN 64u   /* ... left a query uncertified: the batch ran again, thresholded */
 
 /* Per-kernel timing (BSR_FLAG_PROFILE): cumulative device milliseconds and launch counts
  * since the last reset, measured with hipEvents on the index's stream. */

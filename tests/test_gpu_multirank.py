@@ -333,19 +333,19 @@ def test_rccl_forced_collectives_single_rank(bsr_mod, oracle_mod, gpu, corpus, m
     for rep in range(2):
         got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
         st = ix.last_stats()
-        assert st.parallel_path & gt_bits == gt_bits, (rep, st.parallel_path)
+        assert st.search_path & gt_bits == gt_bits, (rep, st.search_path)
         assert st.n_candidates == 0 and st.n_fallback == 0, (st.n_candidates, st.n_fallback)
         _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
     # 2. the root's outputs in coherent pinned memory: the merge writes them directly
     r = _search_into_host_arrays(bsr_mod, comm, ix, q, mr_worker.K)
-    assert ix.last_stats().parallel_path == gt_bits | P.BSR_PATH_DIRECT_OUT, ix.last_stats().parallel_path
+    assert ix.last_stats().search_path == gt_bits | P.BSR_PATH_DIRECT_OUT, ix.last_stats().search_path
     _same(r, want)
     # 3. no merged list certifies: every query's rows come from the collective fallback (the
     # standard path's RCCL group and device merge), patched into the direct outputs
     monkeypatch.setenv("BSR_INJECT_FAULT", "gtau_uncertified")
     r = _search_into_host_arrays(bsr_mod, comm, ix, q, mr_worker.K)
     st = ix.last_stats()
-    assert st.parallel_path == gt_bits | P.BSR_PATH_DIRECT_OUT | P.BSR_PATH_FALLBACK, st.parallel_path
+    assert st.search_path == gt_bits | P.BSR_PATH_DIRECT_OUT | P.BSR_PATH_FALLBACK, st.search_path
     assert st.n_fallback == len(q)
     _same(r, want)
     # 4. phase A fails after the header (poisoned contribution): every query through the fallback,
@@ -353,23 +353,23 @@ def test_rccl_forced_collectives_single_rank(bsr_mod, oracle_mod, gpu, corpus, m
     monkeypatch.setenv("BSR_INJECT_FAULT", "phase_a1")
     got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
     st = ix.last_stats()
-    assert st.parallel_path & P.BSR_PATH_FALLBACK and st.n_fallback == len(q), (st.parallel_path, st.n_fallback)
+    assert st.search_path & P.BSR_PATH_FALLBACK and st.n_fallback == len(q), (st.search_path, st.n_fallback)
     _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
     monkeypatch.delenv("BSR_INJECT_FAULT")
     # 5. the standard path: header from the search's hook, the group of three all-gathers, the
     # device merge -- a 40-query batch with the global threshold off, and a 5-query batch (<= 16)
     monkeypatch.setenv("BSR_GLOBAL_TAU", "0")
     got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
-    assert ix.last_stats().parallel_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
+    assert ix.last_stats().search_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
     _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
     monkeypatch.delenv("BSR_GLOBAL_TAU")
     small = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q[:5], mr_worker.K)
-    assert ix.last_stats().parallel_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
+    assert ix.last_stats().search_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
     _same({"idx": small[0], "dist": small[1], "cnt": small[2]}, _want(oracle_mod, rows, q[:5]))
     # 6. without the switch a one-rank communicator skips the collectives (the local lists)
     monkeypatch.delenv("BSR_FORCE_COLLECTIVES")
     got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
-    assert ix.last_stats().parallel_path == 0
+    assert ix.last_stats().search_path == 0
     _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
     comm.close()
     ix.close()
@@ -400,7 +400,7 @@ def test_rccl_forced_collectives_configs2_shard(bsr_mod, oracle_mod, gpu, monkey
         got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, k)
         st = ix.last_stats()
         bits = bsr_mod.BSR_PATH_COLLECTIVE | bsr_mod.BSR_PATH_GLOBAL_TAU
-        assert st.parallel_path & bits == bits, st.parallel_path
+        assert st.search_path & bits == bits, st.search_path
         assert st.n_fallback <= nq // 200, st.n_fallback
         fs._check_properties(got, n, k, "forced collectives, 1.25M shard")
         for pos, row in plant:

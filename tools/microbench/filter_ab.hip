@@ -5,7 +5,7 @@
 // Build: make -C tools/microbench filter_ab      Run: ./filter_ab [rows] [queries] [rounds] [tau]
 // (tau: 0.1473 emits ~256 rows per query at 10M rows, 0.1284 at 1.25M -- the product's rate)
 #include "k_filter.hip"
-#include "k_rs_lab.hip"
+#include "k_rs_lab.hip"  // (row-streaming lab kernels: kept for reference, not timed)
 
 #include <stdio.h>
 #include <string.h>
@@ -76,10 +76,9 @@ int main(int argc, char** argv) {
     struct V { const char* name; void (*k)(bsr::GemmArgs); std::vector<float> t; int rs = 0; };
     std::vector<V> vs = {
         {"product", bsr::k_filter_qs16<true, 12>, {}},
-        {"rs12r4", bsr::lab::k_filter_rs<12, 4>, {}, 12},
-        {"rs12r6", bsr::lab::k_filter_rs<12, 6>, {}, 12},
-        {"rs16r3b3", bsr::lab::k_filter_rs<16, 3, 3>, {}, 16},
-        {"rs12r4hot", bsr::lab::k_filter_rs<12, 4, 4, 1>, {}, 12},
+        // round 6: the K-split wave pair's bound (timing only, tau = inf is the reading)
+        {"ksb1hot", bsr::k_filter_qs16<true, 12, 0, 8, 2, 0, 0, 1, 1>, {}},
+        {"ksb2hot", bsr::k_filter_qs16<true, 12, 0, 8, 2, 0, 0, 1, 2>, {}},
     };
 
     hipEvent_t e0, e1;
