@@ -87,6 +87,17 @@ for step in $STEPS; do
               "$O/p50ab_${v}_$r.json" "$v"
         done
       done ;;
+    p50top)
+      # round 6: the self-thresholded single-query path on / off, interleaved in one process
+      run 400 "p50top" "$O/p50top.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200; cat "$O/p50top.txt" ;;
+    toptests)
+      # round 6: the new collective and single-query tests alone
+      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+        tests/test_gpu_tiny_top.py tests/test_gpu_multirank.py::test_rccl_forced_collectives_single_rank \
+        tests/test_gpu_multirank.py::test_rccl_forced_collectives_configs2_shard \
+        tests/test_gpu_multirank.py::test_parallel_search_phase_a_faults \
+        "tests/test_gpu_parity.py::test_published_rescue_and_fallback_rows" > "$O/toptests.log" 2>&1
+      rc=$?; echo "toptests rc=$rc"; tail -25 "$O/toptests.log"; [ $rc -eq 0 ] || exit $rc ;;
     p50rs)
       # the single-query rescore kernels, kp on / off, two rounds (tools/diag/p50_rescore.py)
       for r in 1 2; do
