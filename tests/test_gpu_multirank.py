@@ -366,10 +366,11 @@ def test_rccl_forced_collectives_single_rank(bsr_mod, oracle_mod, gpu, corpus, m
     small = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q[:5], mr_worker.K)
     assert ix.last_stats().search_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
     _same({"idx": small[0], "dist": small[1], "cnt": small[2]}, _want(oracle_mod, rows, q[:5]))
-    # 6. without the switch a one-rank communicator skips the collectives (the local lists)
+    # 6. without the switch a one-rank communicator skips the header and the global threshold: the
+    # local search, then the standard exchange (one rank's lists) and the device merge
     monkeypatch.delenv("BSR_FORCE_COLLECTIVES")
     got = bsr_mod.parallel_top_k_similarity_search_batch(comm, ix, q, mr_worker.K)
-    assert ix.last_stats().search_path == 0
+    assert ix.last_stats().search_path == P.BSR_PATH_COLLECTIVE | P.BSR_PATH_DEVICE_MERGE
     _same({"idx": got[0], "dist": got[1], "cnt": got[2]}, want)
     comm.close()
     ix.close()

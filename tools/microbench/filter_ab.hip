@@ -79,6 +79,10 @@ int main(int argc, char** argv) {
         // round 6: the K-split wave pair's bound (timing only, tau = inf is the reading)
         {"ksb1hot", bsr::k_filter_qs16<true, 12, 0, 8, 2, 0, 0, 1, 1>, {}},
         {"ksb2hot", bsr::k_filter_qs16<true, 12, 0, 8, 2, 0, 0, 1, 2>, {}},
+        // round 6: the small-shard build (what launch_filter takes below ~5.6M rows) with one tail
+        // counter per query tile (the product) and with the XCD-local tail pools
+        {"small", bsr::k_filter_qs16<true, 12, 0, 0, 0, 0, 1, 0>, {}},
+        {"smallx", bsr::k_filter_qs16<true, 12, 0, 8, 0, 0, 1, 0>, {}},
     };
 
     hipEvent_t e0, e1;
