@@ -418,8 +418,8 @@ static uint32_t top_slots(const bsr_index* ix, uint32_t nq, uint32_t k) {
     if (nq > kSkinnyMaxQ || ix->n < kSkinnyTopMinRows || kp_for(k) > 63 || k > 64 || ix->op_row_bytes > 16 * 64 ||
         ix->ld % 64 != 0 || ix->ld > 1024 || !rescore_kp_enabled())
         return 0;
-    const uint32_t slots = 4 * skinny_top_waves((uint32_t)ix->n);
-    return slots <= 16u * ix->ld ? slots : 0;  // (k_rescore_kp holds 16 keys per lane)
+    const uint32_t slots = 4 * skinny_top_lists((uint32_t)ix->n);
+    return slots <= 64u * kTopKeysPerLane ? slots : 0;  // (k_rescore_kp's wave 0 holds the lists)
 }
 
 // Buffers of the candidate stage for a batch (k' = kp_for(k) candidates, lists of cap keys).
@@ -530,6 +530,7 @@ static int top_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cnt = ix->cnt.as<uint32_t>();
     g.cap = top_slots(ix, nq, k);
     g.status = ix->d_status;
+    g.n_q = nq;
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return launch_filter_skinny_top(g, ix->stream, e0, e1);
     }));
@@ -595,7 +596,7 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
         ra.tau0 = ix->tau.as<float>();
     }
     if (top) {
-        ra.top_w = top / 4;
+        ra.top_w = top / 4;  // (lists: one per workgroup of the skinny filter)
         ra.qflags = ix->qflags.as<uint32_t>();
         ra.top_tau = ix->tau.as<float>();  // (the second chance's tau0)
         ra.top_cnt = ix->cnt.as<uint32_t>();

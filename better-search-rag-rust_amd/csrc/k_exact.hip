@@ -143,14 +143,17 @@ __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 // compacted through lsel (LDS, 64 words): lane l's row in sel_row (l < c on return).  tx_sel: the
 // (kp+1)-th score (every row left out is at most that), or tau0 when every emitted row is a
 // candidate; INFINITY for an overflowed list.
-__device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c, bool overflow, uint32_t kp,
-                                          float tau0, float& tx_sel, uint32_t* lsel, uint32_t& sel_row, int lane) {
-    constexpr int NR = 16;
+// (select_kp_n<NR>: NR keys per lane; sparse = true: the kKeyNone slots may lie anywhere among
+// the first slots -- c counts the valid keys, each slot is masked by its own key, not its index)
+template <int NR>
+__device__ __forceinline__ void select_kp_n(const uint64_t (&xk)[NR], uint32_t& c, bool overflow, uint32_t kp,
+                                            float tau0, float& tx_sel, uint32_t* lsel, uint32_t& sel_row, int lane,
+                                            bool sparse = false) {
     uint64_t x[NR];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
         const uint32_t i = j * kWave + lane;
-        x[j] = i < c ? xk[j] : kKeyNone;
+        x[j] = (sparse || i < c) ? xk[j] : kKeyNone;
     }
     uint64_t T = kKeyNone;
     if (!overflow && c > kp) {
@@ -173,13 +176,13 @@ __device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c,
             uint32_t below = 0;
 #pragma unroll
             for (int j = 0; j < NR; ++j)
-                if (j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
+                if (sparse || j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
             if (below < K) Th = t;
         }
         uint32_t lt = 0, eq = 0;
 #pragma unroll
         for (int j = 0; j < NR; ++j)
-            if (j * kWave < (int)c) {
+            if (sparse || j * kWave < (int)c) {
                 const uint32_t h = (uint32_t)(x[j] >> 32);
                 lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
                 eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
@@ -192,7 +195,7 @@ __device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c,
                 uint32_t below = 0;
 #pragma unroll
                 for (int j = 0; j < NR; ++j)
-                    if (j * kWave < (int)c)
+                    if (sparse || j * kWave < (int)c)
                         below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
                 if (below < K2) Tl = t;
             }
@@ -223,6 +226,11 @@ __device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c,
     wave_sync();
     sel_row = lane < (int)c ? lsel[lane] : 0u;
     wave_sync();
+}
+
+__device__ __forceinline__ void select_kp(const uint64_t (&xk)[16], uint32_t& c, bool overflow, uint32_t kp,
+                                          float tau0, float& tx_sel, uint32_t* lsel, uint32_t& sel_row, int lane) {
+    select_kp_n<16>(xk, c, overflow, kp, tau0, tx_sel, lsel, sel_row, lane);
 }
 
 // Certification: every row outside the candidate set has approximate cosine
@@ -669,54 +677,32 @@ __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
 // arithmetic and its order are k_rescore's, so the distances are its bits; wave 0 finishes
 // (top-k, certification, result rows) as k_rescore mode S does.  One-wave k_rescore spent ~30 us
 // on one query's 63 rows: 12 chunks, each behind its own load latency.
-// The self-thresholded path's selection (RescoreArgs::top_w), every wave of the workgroup: the
-// query's 4 * top_w keys (ascending 4-lists, one per wave of the skinny filter) in registers,
-// JU per lane; the bound X of the rows outside the lists (the smallest 4th key: every row a wave
-// left out scores at most its 4th); a block-wide radix select of the (kp+1)-th smallest key T
-// (high words first, then -- only when several keys share T's high word -- the low words), the
-// kp keys below it compacted into lsel.  tau_x = max(score(T), score(X)): every row outside the
-// candidates scores at most that.  The keys below X are then compacted to the front of the
-// query's list for the second chance (certified against score(X)).
-template <int JU>
-__device__ __forceinline__ void top_select_t(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c,
-                                             float& s_tx, uint32_t& s_ov, int w, int nw, int lane) {
-    __shared__ uint32_t s_cnt[2][16];
-    __shared__ uint64_t s_x[16];
-    __shared__ uint32_t s_pos, s_pos2, s_tl;
-    const uint32_t U = 4 * a.top_w, stride = (uint32_t)nw * 64;
+// The self-thresholded path's selection (RescoreArgs::top_w), wave 0 of k_rescore_kp: the query's
+// 4 * top_w keys (ascending 4-lists, one per workgroup of the skinny filter) in registers; the
+// bound X of the rows outside the lists -- the smallest 4th key: every row a workgroup left out
+// scores at most its 4th --; select_kp's radix select of the (kp+1)-th smallest key, the kp keys
+// below it compacted into lsel.  tau_x = max(that score, score(X)): every row outside the
+// candidates scores at most that.  Then the keys below X go to the front of the query's list,
+// their count to top_cnt and score(X) to top_tau: the second chance's input.
+__device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c,
+                                           float& s_tx, uint32_t& s_ov, int lane) {
+    constexpr int NR = (int)kTopKeysPerLane;
+    const uint32_t U = 4 * a.top_w;
     const bool served = !(a.qflags[q] & kQueryNoApprox);
     uint64_t* const list = const_cast<uint64_t*>(a.cand_keys) + (uint64_t)q * a.cap;
-    uint64_t x[JU];
+    uint64_t xk[NR];
 #pragma unroll
-    for (int j = 0; j < JU; ++j) {
-        const uint32_t i = j * stride + (uint32_t)w * 64 + lane;
-        x[j] = (served && i < U) ? list[i] : kKeyNone;
+    for (int j = 0; j < NR; ++j) {
+        const uint32_t i = j * kWave + lane;
+        xk[j] = (served && i < U) ? list[i] : kKeyNone;
     }
-    if (threadIdx.x == 0) { s_pos = 0; s_pos2 = 0; }
-    int par = 0;
-    // block-wide count of the keys satisfying pred (one barrier)
-    auto count = [&](auto pred) -> uint32_t {
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < JU; ++j) c += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && pred(x[j])));
-        if (lane == 0) s_cnt[par][w] = c;
-        __syncthreads();
-        uint32_t t = 0;
-        for (int v = 0; v < nw; ++v) t += s_cnt[par][v];
-        par ^= 1;
-        return t;
-    };
-    // X: the smallest of the lists' 4th keys (list slot 3: lanes with lane % 4 == 3, as 64 nw is
-    // a multiple of 4); the high-word range of the valid keys
+    // X: the smallest of the lists' 4th keys (slot 3 of each list: lanes with lane % 4 == 3)
     uint64_t mx = kKeyNone;
-    uint32_t hmin = ~0u, hmax = 0;
+    uint32_t V = 0;  // valid keys
 #pragma unroll
-    for (int j = 0; j < JU; ++j) {
-        if ((lane & 3) == 3) mx = x[j] < mx ? x[j] : mx;
-        if (x[j] != kKeyNone) {
-            hmin = min(hmin, (uint32_t)(x[j] >> 32));
-            hmax = max(hmax, (uint32_t)(x[j] >> 32));
-        }
+    for (int j = 0; j < NR; ++j) {
+        if ((lane & 3) == 3) mx = xk[j] < mx ? xk[j] : mx;
+        V += (uint32_t)__popcll(__ballot(xk[j] != kKeyNone));
     }
     {
         uint32_t lo = (uint32_t)mx, hi = (uint32_t)(mx >> 32);
@@ -729,76 +715,30 @@ __device__ __forceinline__ void top_select_t(const RescoreArgs& a, uint32_t q, u
         }
         mx = ((uint64_t)hi << 32) | lo;
     }
-    hmin = wave_reduce_u32(hmin, [](uint32_t u, uint32_t v) { return min(u, v); });
-    hmax = wave_reduce_u32(hmax, [](uint32_t u, uint32_t v) { return max(u, v); });
-    if (lane == 0) {
-        s_x[w] = mx;
-        s_cnt[0][w] = hmin;
-        s_cnt[1][w] = hmax;
-    }
-    __syncthreads();
-    uint64_t X = kKeyNone;
-    hmin = ~0u;
-    hmax = 0;
-    for (int v = 0; v < nw; ++v) {
-        X = s_x[v] < X ? s_x[v] : X;
-        hmin = min(hmin, s_cnt[0][v]);
-        hmax = max(hmax, s_cnt[1][v]);
-    }
-    __syncthreads();  // (s_cnt is the count buffer from here)
+    const uint64_t X = mx;
     const float tx_trunc = X == kKeyNone ? -INFINITY : score_key_score(X);
-    const uint32_t K = a.kp + 1;
-    const uint32_t V = count([](uint64_t) { return true; });
-    uint64_t T = kKeyNone;
-    float tx = tx_trunc;
-    if (V > a.kp) {
-        const uint32_t diff = hmin ^ hmax;
-        const int top = diff ? 31 - __builtin_clz(diff) : -1;
-        uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
-        for (int b = top; b >= 0; --b) {
-            const uint32_t t = Th | (1u << b);
-            if (count([t](uint64_t k) { return (uint32_t)(k >> 32) < t; }) < K) Th = t;
-        }
-        const uint32_t lt = count([Th](uint64_t k) { return (uint32_t)(k >> 32) < Th; });
-        const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
-        const uint32_t eq = count([Th](uint64_t k) { return (uint32_t)(k >> 32) == Th; });
-        uint32_t Tl = 0;
-        if (eq > 1) {
-            for (int b = 31; b >= 0; --b) {
-                const uint32_t t = Tl | (1u << b);
-                if (count([Th, t](uint64_t k) { return (uint32_t)(k >> 32) == Th && (uint32_t)k < t; }) < K2) Tl = t;
-            }
-        } else {  // the one key with high word Th (keys are unique: the row is the low word)
+    // the second chance's input first (select_kp compacts in place): the keys below X, in order
+    uint32_t base = 0;
 #pragma unroll
-            for (int j = 0; j < JU; ++j)
-                if (x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th) s_tl = (uint32_t)x[j];
-            __syncthreads();
-            Tl = s_tl;
-        }
-        T = ((uint64_t)Th << 32) | Tl;
-        tx = fmaxf(score_key_score(T), tx_trunc);
+    for (int j = 0; j < NR; ++j) {
+        const bool pick = xk[j] < X;  // (kKeyNone never: it is no smaller than X)
+        const uint64_t m = __ballot(pick);
+        if (pick) list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = xk[j];
+        base += (uint32_t)__popcll(m);
     }
-    // the candidates: every valid key below T (all of them when V <= kp), compacted into lsel
-#pragma unroll
-    for (int j = 0; j < JU; ++j)
-        if (x[j] != kKeyNone && x[j] < T) lsel[atomicAdd(&s_pos, 1u)] = key_row(x[j]);
-    __syncthreads();  // (every key was read from the list above: it may be rewritten now)
-    // the second chance's input: the keys below X at the front of the list, their count
-#pragma unroll
-    for (int j = 0; j < JU; ++j)
-        if (x[j] != kKeyNone && x[j] < X) list[atomicAdd(&s_pos2, 1u)] = x[j];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s_c = s_pos;
-        s_tx = served ? tx : INFINITY;
+    // the k' candidates: keys are unique (the row is the low word), kKeyNone slots are dropped by
+    // select_kp's count c (it takes the first c slots as valid: move the valid keys first)
+    uint32_t c = V;
+    float tx = tx_trunc;
+    uint32_t sel_row = 0;
+    select_kp_n<NR>(xk, c, false, a.kp, tx_trunc, tx, lsel, sel_row, lane, true);
+    if (lane == 0) {
+        s_c = c;
+        s_tx = served ? fmaxf(tx, tx_trunc) : INFINITY;
         s_ov = served ? 0u : 1u;
-        a.top_cnt[q] = s_pos2;
+        a.top_cnt[q] = base;
         a.top_tau[q] = served ? tx_trunc : INFINITY;
     }
-}
-__device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c, float& s_tx,
-                                           uint32_t& s_ov, int w, int nw, int lane) {
-    top_select_t<16>(a, q, lsel, s_c, s_tx, s_ov, w, nw, lane);
 }
 
 // ------------------------------------------------------------------------------------
@@ -820,7 +760,7 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     // the query's chunk of this wave, staged in LDS (read as broadcasts)
     if ((uint32_t)(w * 64 + lane) < ld) ldq[w * 64 + lane] = a.qf32[(uint64_t)q * ld + w * 64 + lane];
     if (a.top_w) {
-        top_select(a, q, lsel, s_c, s_tx, s_ov, w, nw, lane);
+        if (w == 0) top_select(a, q, lsel, s_c, s_tx, s_ov, lane);
     } else if (w == 0) {
         constexpr int NR = 16;
         uint64_t xk[NR];
@@ -1399,7 +1339,7 @@ hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     // (BSR_RESCORE_KP=0: the one-wave kernel instead, for A/B runs)
     static const bool kp_on = rescore_kp_enabled();
     if (a.top_w && !(kp_on && a.n_items <= 16 && a.ld % 64 == 0 && a.ld <= 1024 && a.k <= 64 && a.kp <= 63 &&
-                     4 * a.top_w <= 16u * (a.ld / 64) * 64))
+                     4 * a.top_w <= 64u * kTopKeysPerLane))
         return hipErrorInvalidValue;  // (the self-thresholded path needs k_rescore_kp: the caller checks)
     if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && a.n_items <= 16 && a.ld % 64 == 0 &&
         a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && (a.cap <= 1024 || a.top_w)) {

@@ -1336,9 +1336,10 @@ __global__ __launch_bounds__(256) void k_filter_skinny(GemmArgs p) {
 // SAMPLE: a wave takes the two units of one 32-sampled-row block back to back, so the
 // compact maximum over 32 sampled rows stays in a register.
 // TOP (round 6, the self-thresholded single-query path): units dealt as EMIT, no threshold;
-// each lane keeps the 4 best (score, row) keys of its rows, the four lanes of a query merge
-// them at the end, and the wave writes its 4 best keys per query to cand[q][wave][4] -- every
-// row of the wave not among them scores at most its 4th (tiny batches).
+// each lane keeps the 4 best (score, row) keys of its rows, the four lanes of a query and then
+// the workgroup's four waves merge them at the end, and the workgroup writes its 4 best keys per
+// query to cand[q][workgroup][4] -- every row of the workgroup not among them scores at most its
+// 4th (tiny batches).
 // ------------------------------------------------------------------------------------
 #ifndef BSR_SKINNY_NT
 #define BSR_SKINNY_NT 0
@@ -1361,7 +1362,9 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     const uint32_t q = lane & 15, h = lane >> 4;
     const uint32_t nk = p.row_bytes / kSliceB;
     const uint32_t n_units = (p.n_rows + 15) / 16;
-    const uint32_t nwaves = gridDim.x * 4, wid = blockIdx.x * 4 + w;
+    // (TOP: the workgroup's waves take units gridDim.x apart, so that the rows of a run of
+    // consecutive units -- a cluster of similar rows, below -- fall into different workgroups)
+    const uint32_t nwaves = gridDim.x * 4, wid = TOP ? w * gridDim.x + blockIdx.x : blockIdx.x * 4 + w;
     const float sbq = p.b_scale[q];
     const float tauq = EMIT ? p.tau[q] : 0.0f;
     i32x4_t fb[NK];
@@ -1376,15 +1379,16 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     // TOP: the lane's 4 best keys (ascending) and the score of the 4th (-inf until it has 4)
     uint64_t tk[4] = {kKeyNone, kKeyNone, kKeyNone, kKeyNone};
     float tk3 = -INFINITY;
+    const bool live = !TOP || q < p.n_q;  // (TOP: padding queries keep no list)
     if (TOP && blockIdx.x == 0 && threadIdx.x < 16) {
         // (the bookkeeping k_select_tau does on the thresholded path: every query's list is
-        // its 4 * nwaves slots, the status words of the rescores that follow start at 0)
-        p.cnt[threadIdx.x] = 4 * nwaves;
+        // its 4 * gridDim.x slots, the status words of the rescores that follow start at 0)
+        p.cnt[threadIdx.x] = 4 * gridDim.x;
         if (threadIdx.x == 0) { p.status[kStFail] = 0; p.status[kStEmitted] = 0; p.status[kStFail2] = 0; }
     }
     // TOP: unit u holds the strided rows u, u + n_units, ..., u + 15 n_units (A-row m = row
     // m n_units + u), so a run of consecutive similar rows is spread over consecutive units, i.e.
-    // over different waves: no wave's 4 best are all from one cluster unless it spans > 2048 rows
+    // over different workgroups: no workgroup's 4 best come from one cluster of up to ~gridDim rows
     auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t { return TOP ? m * n_units + u : u * 16 + m; };
     auto load = [&](i32x4_t (&fa)[NK], uint32_t u) {
         uint32_t r = row_of(u, q);
@@ -1407,20 +1411,28 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
             if (s < (int)nk) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
         // register i: tile row u*16 + 4h + i, query q
         if constexpr (TOP) {
+            // the block scale of the row this lane loaded (A-row q), then of its output rows
+            // 4h + i, taken from the lanes that loaded them (lane 16h + 4h + i: same h, q = 4h + i)
+            const uint32_t rq = row_of(u, q);
+            const float sc_own = p.a_scale[(rq < p.n_rows ? rq : p.n_rows - 1) / kQuantBlock];
             float v[4];
-            uint32_t rw[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                rw[i] = row_of(u, 4 * h + i);
-                const float sc = p.a_scale[(rw[i] < p.n_rows ? rw[i] : p.n_rows - 1) / kQuantBlock];
+                const float sc = __shfl(sc_own, (int)(16 * h + 4 * h + i), kWave);
                 v[i] = ((float)acc[i] * sc) * sbq;
             }
             const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-            if (mx >= tk3) {  // (rare once the lane holds 4 keys: ~4 ln(rows / 4) insertions)
+            // (strictly above the lane's 4th: a row at most its 4th stays within the bound; rare
+            // once the lane holds 4 keys, ~4 ln(rows / 4) insertions)
+            if (live && mx > tk3) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (rw[i] < p.n_rows) top4_insert(tk, score_key(v[i], rw[i]));
-                tk3 = tk[3] == kKeyNone ? -INFINITY : score_key_score(tk[3]);
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t rw = row_of(u, 4 * h + i);
+                    if (v[i] > tk3 && rw < p.n_rows) {
+                        top4_insert(tk, score_key(v[i], rw));
+                        tk3 = tk[3] == kKeyNone ? -INFINITY : score_key_score(tk[3]);
+                    }
+                }
             }
         } else if constexpr (EMIT) {
             const float sc = p.a_scale[(u * 16) / kQuantBlock];
@@ -1494,8 +1506,19 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) top4_insert(tk, o[j]);
         }
-        if (h == 0) {
-            uint64_t* dst = p.cand + ((uint64_t)q * nwaves + wid) * 4;
+        // the workgroup's four waves: wave 0 merges the others' lists (LDS) and writes the
+        // workgroup's 4 best keys of each query
+        __shared__ uint64_t wl[4][16][4];
+        if (h == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wl[w][q][j] = tk[j];
+        __syncthreads();
+        if (w == 0 && h == 0) {
+#pragma unroll
+            for (int o = 1; o < 4; ++o)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) top4_insert(tk, wl[o][q][j]);
+            uint64_t* dst = p.cand + ((uint64_t)q * gridDim.x + blockIdx.x) * 4;
 #pragma unroll
             for (int j = 0; j < 4; ++j) dst[j] = tk[j];
         }
@@ -1827,7 +1850,7 @@ static uint32_t skinny2_grid(uint32_t n_rows) {
     const uint32_t units = (n_rows + 15) / 16;
     return std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
 }
-uint32_t skinny_top_waves(uint32_t n_rows) { return 4 * skinny2_grid(n_rows); }
+uint32_t skinny_top_lists(uint32_t n_rows) { return skinny2_grid(n_rows); }
 template <int MODE>
 static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB;

@@ -99,8 +99,10 @@ struct GemmArgs {
     // to the workgroups' row streams round-robin, the rest are claimed one at a time per query
     // tile from tail[qt] (zeroed by k_select_tau); tail = nullptr: every tile static
     uint32_t* tail;
-    // skinny TOP: the search's status words (zeroed by the kernel: no k_select_tau runs)
+    // skinny TOP: the search's status words (zeroed by the kernel: no k_select_tau runs) and
+    // the batch's query count (padding queries keep no list)
     uint32_t* status;
+    uint32_t n_q;
 };
 // Dynamic tail of the emit filter: 1/kTailDiv of the row tiles; counters per (XCD pool, query
 // tile) (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + x * n_qt + qt].
@@ -127,13 +129,13 @@ constexpr uint32_t kSkinnyMaxQ = 16;
 hipError_t launch_filter_skinny_sample(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // The self-thresholded single-query path (round 6; rows of <= 16 K slices): no sample pass and no
-// tau0 -- each of the skinny2 grid's W = skinny_top_waves(n) waves writes its 4 best keys per
-// query to cand[q][W][4] (ascending; every other row of the wave scores at most the 4th), and
+// tau0 -- each of the skinny2 grid's W = skinny_top_lists(n) workgroups writes its 4 best keys per
+// query to cand[q][W][4] (ascending; every other row of the workgroup scores at most the 4th), and
 // cnt[q] = 4 W for q < 16; the status words kStFail / kStEmitted / kStFail2 are zeroed.
 hipError_t launch_filter_skinny_top(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-uint32_t skinny_top_waves(uint32_t n_rows);
+uint32_t skinny_top_lists(uint32_t n_rows);
 // Shards of at least this many rows take the self-thresholded path for batches of <= 16 queries
-// and k' <= 63 (every wave of the 2048-wave grid then holds >= 64 units of 16 rows).
+// and k' <= 63 (every wave of the 512-workgroup grid then holds >= 64 units of 16 rows).
 constexpr uint64_t kSkinnyTopMinRows = 2u << 20;
 
 // tau[q] = the ks-th best sampled score (ks <= 128); also zeroes cnt[0..qpad) and the status
@@ -182,9 +184,8 @@ struct RescoreArgs {
     // or tau0 when fewer were emitted) -- k_select_cand is not launched
     uint32_t sel;
     // mode S of the self-thresholded single-query path (top_w != 0; the tiny-batch kernel
-    // k_rescore_kp only): cand_keys[q * cap ..] holds top_w ascending 4-lists (cap = 4 top_w,
-    // launch_filter_skinny_top); every wave of the workgroup takes part in the radix select of
-    // the k' best of them.  The bound on the rows outside the lists -- the best score among the
+    // k_rescore_kp only): cand_keys[q * cap ..] holds top_w ascending 4-lists (cap = 4 top_w <=
+    // 64 kTopKeysPerLane, launch_filter_skinny_top); its wave 0 radix-selects the k' best of them.  The bound on the rows outside the lists -- the best score among the
     // lists' 4th keys -- goes to top_tau[q], and the keys above it are compacted to the front of
     // the query's list, their count to top_cnt[q]: the second chance's mode-B input (a query the
     // filter cannot serve: count 0, bound +inf).
@@ -247,6 +248,8 @@ constexpr uint32_t kFusedSelectCap = 1024;
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s);
 // whether launch_rescore takes k_rescore_kp for a tiny batch's first pass (BSR_RESCORE_KP != 0)
 bool rescore_kp_enabled();
+// The self-thresholded path's lists per query are selected by one wave, this many keys per lane.
+constexpr uint32_t kTopKeysPerLane = 32;
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold
 // grid * kScanQF * k keys.
 hipError_t launch_scan_exact(const float* rows, uint32_t ld, uint32_t dim, uint64_t n,
