@@ -531,6 +531,8 @@ static int top_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cap = top_slots(ix, nq, k);
     g.status = ix->d_status;
     g.n_q = nq;
+    const char* lay = getenv("BSR_TOP_LAYOUT");  // (lab A/B only: the product layout is 1)
+    g.top_layout = lay ? (uint32_t)atoi(lay) & 3u : 1u;
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return launch_filter_skinny_top(g, ix->stream, e0, e1);
     }));

@@ -1389,7 +1389,15 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     // TOP: unit u holds the strided rows u, u + n_units, ..., u + 15 n_units (A-row m = row
     // m n_units + u), so a run of consecutive similar rows is spread over consecutive units, i.e.
     // over different workgroups: no workgroup's 4 best come from one cluster of up to ~gridDim rows
-    auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t { return TOP ? m * n_units + u : u * 16 + m; };
+    // (lab, round 6: p.top_layout 0 = contiguous units as EMIT, 2 = eight strided pairs, 3 = four
+    // strided quads -- the HBM pattern against the clusters' spread; 1 = the sixteen strided rows)
+    const uint32_t lay = TOP ? p.top_layout : 0u;
+    auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
+        if (!TOP || lay == 0) return u * 16 + m;
+        if (lay == 2) return (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
+        if (lay == 3) return (m >> 2) * (4 * n_units) + 4 * u + (m & 3);
+        return m * n_units + u;
+    };
     auto load = [&](i32x4_t (&fa)[NK], uint32_t u) {
         uint32_t r = row_of(u, q);
         r = r < p.n_rows ? r : p.n_rows - 1;  // tail rows: clamped, never emitted

@@ -45,9 +45,15 @@ def main():
     t_end = time.time() + 1.0
     while time.time() < t_end:  # settle the clock
         one(1)
+    modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["1", "0"]
     for r in range(rounds):
-        for mode in ("1", "0"):
-            os.environ["BSR_SKINNY_TOP"] = mode
+        for mode in modes:
+            # "0": the thresholded path; "1": the self-thresholded path; "1:L": with the lab row layout L
+            os.environ["BSR_SKINNY_TOP"] = mode[0]
+            if ":" in mode:
+                os.environ["BSR_TOP_LAYOUT"] = mode.split(":")[1]
+            else:
+                os.environ.pop("BSR_TOP_LAYOUT", None)
             for _ in range(20):
                 one(1)
             lat = []
@@ -66,11 +72,15 @@ def main():
             print(f"round {r} top={mode}: p50 {statistics.median(lat):.4f} ms  min {min(lat):.4f}  "
                   f"path {st.search_path} replay {st.graph_replay} fallback {st.n_fallback} rescued {st.n_rescued} "
                   f"emitted {st.n_emitted}", flush=True)
-    same = all(np.array_equal(a, b) for x, y in zip(res["1"], res["0"]) for a, b in zip(x, y))
-    print(f"results of the two paths over 8 queries: {'IDENTICAL' if same else 'DIFFER'}", flush=True)
+    same = all(np.array_equal(a, b) for m in modes for x, y in zip(res[modes[0]], res[m]) for a, b in zip(x, y))
+    print(f"results of the {len(modes)} paths over 8 queries: {'IDENTICAL' if same else 'DIFFER'}", flush=True)
     # kernel times per mode (profile level 1: the filter events; level 2 every stage)
-    for mode in ("1", "0"):
-        os.environ["BSR_SKINNY_TOP"] = mode
+    for mode in modes:
+        os.environ["BSR_SKINNY_TOP"] = mode[0]
+        if ":" in mode:
+            os.environ["BSR_TOP_LAYOUT"] = mode.split(":")[1]
+        else:
+            os.environ.pop("BSR_TOP_LAYOUT", None)
         ix.set_profile(2)
         ix.profile(reset=True)
         for _ in range(20):

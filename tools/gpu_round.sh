@@ -89,7 +89,7 @@ for step in $STEPS; do
       done ;;
     p50top)
       # round 6: the self-thresholded single-query path on / off, interleaved in one process
-      run 400 "p50top" "$O/p50top.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200; cat "$O/p50top.txt" ;;
+      run 400 "p50top" "$O/p50top.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200 ${P50MODES:-1,0}; cat "$O/p50top.txt" ;;
     toptests)
       # round 6: the new collective and single-query tests alone
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
