@@ -518,6 +518,12 @@ static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     return BSR_OK;
 }
 
+// (lab A/B only: the skinny TOP row layout, BSR_TOP_LAYOUT; the product layout is 1)
+static uint32_t top_layout_lab() {
+    const char* lay = getenv("BSR_TOP_LAYOUT");
+    return lay ? (uint32_t)atoi(lay) & 3u : 1u;
+}
+
 // The self-thresholded filter pass: every wave's 4 best keys per query (launch_filter_skinny_top).
 static int top_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     BSR_TRY(filter_buffers(ix, nq, qpad, k));
@@ -531,8 +537,7 @@ static int top_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     g.cap = top_slots(ix, nq, k);
     g.status = ix->d_status;
     g.n_q = nq;
-    const char* lay = getenv("BSR_TOP_LAYOUT");  // (lab A/B only: the product layout is 1)
-    g.top_layout = lay ? (uint32_t)atoi(lay) & 3u : 1u;
+    g.top_layout = top_layout_lab();
     BSR_HIP(launch_timed(ix, ix->ev_emit, [&](hipEvent_t e0, hipEvent_t e1) {
         return launch_filter_skinny_top(g, ix->stream, e0, e1);
     }));
@@ -775,11 +780,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     if (top) stats.search_path |= BSR_PATH_SKINNY_TOP;
     const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0) && !force_threshold;
     SearchGraph& gs = graphs[cur];
+    const uint32_t lay = top ? top_layout_lab() : 1u;
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
-                            warm.timed == (profiling(ix) ? prof_level : 0) && warm.top == top;
+                            warm.timed == (profiling(ix) ? prof_level : 0) && warm.top == top &&
+                            warm.top_layout == lay;
     const int timed_level = profiling(ix) ? prof_level : 0;
     if (graphable && gs.exec && gs.nq == nq && gs.k == k && gs.qsrc == qsrc && gs.n == n && gs.gen == g_alloc_gen &&
-        gs.timed == timed_level && gs.top == top) {
+        gs.timed == timed_level && gs.top == top && gs.top_layout == lay) {
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         stats.n_candidates = kp_for(k);
         ++graph_replays;
@@ -803,13 +810,13 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(BSR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level, top};
+        gs = SearchGraph{exec, nq, k, qsrc, n, g_alloc_gen, timed_level, top, lay};
         BSR_HIP(hipGraphLaunch(gs.exec, stream));
         ++graph_replays;
         stats.graph_replay = 1;
     } else {
         BSR_TRY(enqueue_search());
-        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, top};
+        if (graphable) warm = SearchGraph{nullptr, nq, k, qsrc, n, g_alloc_gen, timed_level, top, lay};
     }
     next_status_clean = true;
     int hook_st = BSR_OK;
