@@ -518,10 +518,10 @@ static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
     return BSR_OK;
 }
 
-// (lab A/B only: the skinny TOP row layout, BSR_TOP_LAYOUT; the product layout is 1)
+// the skinny TOP row layout: 2, the strided pairs (BSR_TOP_LAYOUT: the lab layouts, A/B only)
 static uint32_t top_layout_lab() {
     const char* lay = getenv("BSR_TOP_LAYOUT");
-    return lay ? (uint32_t)atoi(lay) & 3u : 1u;
+    return lay ? (uint32_t)atoi(lay) & 3u : 2u;
 }
 
 // The self-thresholded filter pass: every wave's 4 best keys per query (launch_filter_skinny_top).
@@ -780,7 +780,7 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     if (top) stats.search_path |= BSR_PATH_SKINNY_TOP;
     const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0) && !force_threshold;
     SearchGraph& gs = graphs[cur];
-    const uint32_t lay = top ? top_layout_lab() : 1u;
+    const uint32_t lay = top ? top_layout_lab() : 2u;
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
                             warm.timed == (profiling(ix) ? prof_level : 0) && warm.top == top &&
                             warm.top_layout == lay;

@@ -125,7 +125,7 @@ struct bsr_index {
         uint64_t n = 0, gen = 0;
         int timed = 0;  // profile level it was captured at (always 0: timed searches launch directly)
         bool top = false;  // the self-thresholded single-query path (round 6)
-        uint32_t top_layout = 1;  // (lab) its row layout (BSR_TOP_LAYOUT, read per search)
+        uint32_t top_layout = 2;  // its row layout (BSR_TOP_LAYOUT, lab: read per search)
     };
     // (round 6) the batch is searched again on the thresholded path: the self-thresholded path
     // left a query uncertified (direct launches, no graph)

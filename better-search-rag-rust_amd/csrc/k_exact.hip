@@ -143,6 +143,59 @@ __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 // compacted through lsel (LDS, 64 words): lane l's row in sel_row (l < c on return).  tx_sel: the
 // (kp+1)-th score (every row left out is at most that), or tau0 when every emitted row is a
 // candidate; INFINITY for an overflowed list.
+// kth_key<NR>: the K-th smallest of the valid keys (kKeyNone = no key; at least K valid) held NR
+// per lane -- the radix search above; only slots j * 64 + lane < dense_c can hold keys (~0u: any).
+template <int NR>
+__device__ __forceinline__ uint64_t kth_key(const uint64_t (&x)[NR], uint32_t K, uint32_t dense_c) {
+    uint32_t hmin = ~0u, hmax = 0;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+        if (x[j] != kKeyNone) {
+            hmin = min(hmin, (uint32_t)(x[j] >> 32));
+            hmax = max(hmax, (uint32_t)(x[j] >> 32));
+        }
+    hmin = wave_reduce_u32(hmin, [](uint32_t a, uint32_t b) { return min(a, b); });
+    hmax = wave_reduce_u32(hmax, [](uint32_t a, uint32_t b) { return max(a, b); });
+    const uint32_t diff = hmin ^ hmax;
+    const int top = diff ? 31 - __builtin_clz(diff) : -1;
+    // (top < 0: every key has the same high word)
+    uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
+    for (int b = top; b >= 0; --b) {
+        const uint32_t t = Th | (1u << b);
+        uint32_t below = 0;
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+            if ((uint32_t)(j * kWave) < dense_c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
+        if (below < K) Th = t;
+    }
+    uint32_t lt = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+        if ((uint32_t)(j * kWave) < dense_c) {
+            const uint32_t h = (uint32_t)(x[j] >> 32);
+            lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
+            eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
+        }
+    const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
+    uint32_t Tl = 0;
+    if (eq > 1)
+        for (int b = 31; b >= 0; --b) {
+            const uint32_t t = Tl | (1u << b);
+            uint32_t below = 0;
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+                if ((uint32_t)(j * kWave) < dense_c)
+                    below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
+            if (below < K2) Tl = t;
+        }
+    else
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {  // the one key with high word Th
+            const uint64_t m = __ballot(x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th);
+            if (m) Tl = (uint32_t)__shfl((int)(uint32_t)x[j], __builtin_ctzll(m), kWave);
+        }
+    return ((uint64_t)Th << 32) | Tl;
+}
 // (select_kp_n<NR>: NR keys per lane; sparse = true: the kKeyNone slots may lie anywhere among
 // the first slots -- c counts the valid keys, each slot is masked by its own key, not its index)
 template <int NR>
@@ -157,55 +210,7 @@ __device__ __forceinline__ void select_kp_n(const uint64_t (&xk)[NR], uint32_t& 
     }
     uint64_t T = kKeyNone;
     if (!overflow && c > kp) {
-        const uint32_t K = kp + 1;
-        uint32_t hmin = ~0u, hmax = 0;
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-            if (x[j] != kKeyNone) {
-                hmin = min(hmin, (uint32_t)(x[j] >> 32));
-                hmax = max(hmax, (uint32_t)(x[j] >> 32));
-            }
-        hmin = wave_reduce_u32(hmin, [](uint32_t a, uint32_t b) { return min(a, b); });
-        hmax = wave_reduce_u32(hmax, [](uint32_t a, uint32_t b) { return max(a, b); });
-        const uint32_t diff = hmin ^ hmax;
-        const int top = diff ? 31 - __builtin_clz(diff) : -1;
-        // (top < 0: every key has the same high word)
-        uint32_t Th = top < 0 ? hmin : top >= 31 ? 0u : (hmin & ~((2u << top) - 1u));
-        for (int b = top; b >= 0; --b) {
-            const uint32_t t = Th | (1u << b);
-            uint32_t below = 0;
-#pragma unroll
-            for (int j = 0; j < NR; ++j)
-                if (sparse || j * kWave < (int)c) below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) < t));
-            if (below < K) Th = t;
-        }
-        uint32_t lt = 0, eq = 0;
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-            if (sparse || j * kWave < (int)c) {
-                const uint32_t h = (uint32_t)(x[j] >> 32);
-                lt += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h < Th));
-                eq += (uint32_t)__popcll(__ballot(x[j] != kKeyNone && h == Th));
-            }
-        const uint32_t K2 = K - lt;  // 1 <= K2 <= eq
-        uint32_t Tl = 0;
-        if (eq > 1)
-            for (int b = 31; b >= 0; --b) {
-                const uint32_t t = Tl | (1u << b);
-                uint32_t below = 0;
-#pragma unroll
-                for (int j = 0; j < NR; ++j)
-                    if (sparse || j * kWave < (int)c)
-                        below += (uint32_t)__popcll(__ballot((uint32_t)(x[j] >> 32) == Th && (uint32_t)x[j] < t));
-                if (below < K2) Tl = t;
-            }
-        else
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {  // the one key with high word Th
-                const uint64_t m = __ballot(x[j] != kKeyNone && (uint32_t)(x[j] >> 32) == Th);
-                if (m) Tl = (uint32_t)__shfl((int)(uint32_t)x[j], __builtin_ctzll(m), kWave);
-            }
-        T = ((uint64_t)Th << 32) | Tl;
+        T = kth_key<NR>(x, kp + 1, sparse ? ~0u : c);
         tx_sel = score_key_score(T);
         c = kp;
     } else if (!overflow) {
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(256) void k_rescore_flat(RescoreArgs a) {
 // candidates scores at most that.  Then the keys below X go to the front of the query's list,
 // their count to top_cnt and score(X) to top_tau: the second chance's input.
 __device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uint32_t* lsel, uint32_t& s_c,
-                                           float& s_tx, uint32_t& s_ov, int lane) {
+                                           float& s_tx, uint32_t& s_ov, int lane, uint64_t* scratch) {
     constexpr int NR = (int)kTopKeysPerLane;
     const uint32_t U = 4 * a.top_w;
     const bool served = !(a.qflags[q] & kQueryNoApprox);
@@ -726,12 +731,54 @@ __device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uin
         if (pick) list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = xk[j];
         base += (uint32_t)__popcll(m);
     }
-    // the k' candidates: keys are unique (the row is the low word), kKeyNone slots are dropped by
-    // select_kp's count c (it takes the first c slots as valid: move the valid keys first)
+    // The k' candidates.  The kp + 1 smallest keys lie among the keys <= H, H the (kp+1)-th smallest
+    // list head (at least kp + 1 keys -- those heads -- are <= H), and only the kp + 1 lists whose
+    // head is <= H hold such keys: at most 4 (kp + 1) of them.  So the radix selects run over the
+    // 512 heads (8 per lane, gathered through LDS) and then those <= 256 keys (4 per lane), not over
+    // all 2048 keys (keys are unique: the row is the low word).
     uint32_t c = V;
     float tx = tx_trunc;
     uint32_t sel_row = 0;
-    select_kp_n<NR>(xk, c, false, a.kp, tx_trunc, tx, lsel, sel_row, lane, true);
+    const uint32_t K = a.kp + 1, nl = a.top_w;
+    uint32_t nh = 0;
+    uint64_t hv[8];
+    if (nl <= 8 * kWave) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+            if ((lane & 3) == 0) scratch[j * 16 + (lane >> 2)] = xk[j];
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t i = t * kWave + lane;
+            hv[t] = i < nl ? scratch[i] : kKeyNone;
+            nh += (uint32_t)__popcll(__ballot(hv[t] != kKeyNone));
+        }
+        wave_sync();
+    }
+    if (nl <= 8 * kWave && nh >= K) {
+        const uint64_t H = kth_key<8>(hv, K, ~0u);
+        uint64_t* const cb = scratch + 8 * kWave;
+        uint32_t C = 0;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const bool pick = xk[j] <= H && xk[j] != kKeyNone;
+            const uint64_t m = __ballot(pick);
+            if (pick) cb[C + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = xk[j];
+            C += (uint32_t)__popcll(m);
+        }
+        wave_sync();
+        uint64_t cv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t i = t * kWave + lane;
+            cv[t] = i < C ? cb[i] : kKeyNone;
+        }
+        wave_sync();
+        c = C;  // (K <= C <= 4 K)
+        select_kp_n<4>(cv, c, false, a.kp, tx_trunc, tx, lsel, sel_row, lane);
+    } else {  // (fewer than kp + 1 lists hold a key: every slot searched)
+        select_kp_n<NR>(xk, c, false, a.kp, tx_trunc, tx, lsel, sel_row, lane, true);
+    }
     if (lane == 0) {
         s_c = c;
         s_tx = served ? fmaxf(tx, tx_trunc) : INFINITY;
@@ -760,7 +807,8 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     // the query's chunk of this wave, staged in LDS (read as broadcasts)
     if ((uint32_t)(w * 64 + lane) < ld) ldq[w * 64 + lane] = a.qf32[(uint64_t)q * ld + w * 64 + lane];
     if (a.top_w) {
-        if (w == 0) top_select(a, q, lsel, s_c, s_tx, s_ov, lane);
+        // (LDS scratch for the heads and candidates: the product stage, first written after this)
+        if (w == 0) top_select(a, q, lsel, s_c, s_tx, s_ov, lane, reinterpret_cast<uint64_t*>(stage));
     } else if (w == 0) {
         constexpr int NR = 16;
         uint64_t xk[NR];

@@ -1386,11 +1386,13 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
         p.cnt[threadIdx.x] = 4 * gridDim.x;
         if (threadIdx.x == 0) { p.status[kStFail] = 0; p.status[kStEmitted] = 0; p.status[kStFail2] = 0; }
     }
-    // TOP: unit u holds the strided rows u, u + n_units, ..., u + 15 n_units (A-row m = row
-    // m n_units + u), so a run of consecutive similar rows is spread over consecutive units, i.e.
-    // over different workgroups: no workgroup's 4 best come from one cluster of up to ~gridDim rows
-    // (lab, round 6: p.top_layout 0 = contiguous units as EMIT, 2 = eight strided pairs, 3 = four
-    // strided quads -- the HBM pattern against the clusters' spread; 1 = the sixteen strided rows)
+    // TOP: unit u holds eight strided pairs of rows, 2u, 2u + 1 of each eighth of the corpus
+    // (A-row m = row (m >> 1) 2 n_units + 2u + (m & 1)), so a run of consecutive similar rows is
+    // spread over consecutive units two at a time, i.e. over different workgroups: no workgroup's 4
+    // best come from one cluster of up to ~2 gridDim rows.  (Lab, p.top_layout: 0 = contiguous
+    // units as EMIT, no spread; 1 = sixteen strided rows; 3 = four strided quads.  p50 over 10M rows
+    // on one box, profiles/r06e_p50_top_layouts.txt: 1.2925 / 1.3092 / 1.3010 ms for layouts 0 / 1 /
+    // 2 against 1.3243 ms for the thresholded path.)
     const uint32_t lay = TOP ? p.top_layout : 0u;
     auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
         if (!TOP || lay == 0) return u * 16 + m;
@@ -1420,7 +1422,8 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
         // register i: tile row u*16 + 4h + i, query q
         if constexpr (TOP) {
             // the block scale of the row this lane loaded (A-row q), then of its output rows
-            // 4h + i, taken from the lanes that loaded them (lane 16h + 4h + i: same h, q = 4h + i)
+            // 4h + i, taken from the lanes that loaded them (lane 16h + 4h + i: same h, q = 4h + i;
+            // two distinct blocks per lane in the pair layout)
             const uint32_t rq = row_of(u, q);
             const float sc_own = p.a_scale[(rq < p.n_rows ? rq : p.n_rows - 1) / kQuantBlock];
             float v[4];
@@ -1889,10 +1892,13 @@ hipError_t launch_filter_skinny_top(const GemmArgs& a, hipStream_t s, hipEvent_t
 // Whether any workgroup of the emit filter can run in a row-stream gang (k_filter_qs16's `gang`
 // condition with its longest static stream).  Otherwise -- every shard of up to ~5.6M rows at 1000
 // queries, and configs[4]'s 16 query tiles -- the launch takes the small-shard build: no gang code
-// (GANG = 0), one tail counter per query tile (TAILX = 0), level 2's bool-array form (L2 = 1) and
-// no explicit wait in the flush (FW = 0): 3-4% faster than the gang build at 1M and 1.25M rows
-// with emission, the same at tau = inf (tools/microbench/filter_hist, profiles/r05c_hist_*,
-// r05e_hist_*).  At 10M the gang build stays: its HBM traffic is 1.1x the rows instead of 2x.
+// (GANG = 0), level 2's bool-array form (L2 = 1) and no explicit wait in the flush (FW = 0): 3-4%
+// faster than the gang build at 1M and 1.25M rows with emission, the same at tau = inf
+// (tools/microbench/filter_hist, profiles/r05c_hist_*, r05e_hist_*).  Round 6: its dynamic tail in
+// the XCD-local pools (TAILX = 8, as the gang build) instead of one counter per query tile -- HBM
+// fetch at the 1.25M-row shard 1.25x -> 1.005x the int8 rows, time within 0.4%
+// (profiles/r06b_fab_125.txt, r06b_fabpmc_1250000.txt: variants "small" / "smallx").  At 10M the
+// gang build stays: its HBM traffic is 1.1x the rows instead of 2x.
 static bool gang_possible(const GemmArgs& a, uint32_t grid) {
     if (!a.tail || a.n_qt < 2 || a.n_qt > 4) return false;
     const uint32_t G = (grid / 8) / a.n_qt, RG = 8 * G;
@@ -1906,7 +1912,7 @@ static void launch_filter(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEv
     if (nk % 2 == 0 && nk <= 12) {
         const dim3 g(grid), b(512);
         if (EMIT && nk == 12 && !gang_possible(a, grid)) {
-            BSR_KLAUNCH((k_filter_qs16<EMIT, 12, 0, 0, 0, 0, 1, 0>), g, b, s, e0, e1, a);
+            BSR_KLAUNCH((k_filter_qs16<EMIT, 12, 0, 8, 0, 0, 1, 0>), g, b, s, e0, e1, a);
             return;
         }
         switch (nk) {

@@ -1,9 +1,9 @@
 """The self-thresholded single-query path (round 6, DESIGN.md §5 tiny batches): a batch of <= 16
 queries over a shard of >= 2^21 rows (k' <= 63, i.e. k <= 10) takes no sample pass and no tau0.
-The skinny filter keeps every wave's 4 best (score, row) keys per query over strided rows; the
-tiny-batch rescore selects the k' best of those 2048 lists with a block-wide radix select, and
-certifies against max(the (k'+1)-th score, the best 4th key) -- every row a wave left out scores
-at most its 4th.  A query that fails takes the second chance (every listed key above that
+The skinny filter keeps every workgroup's 4 best (score, row) keys per query over strided pairs of
+rows; the tiny-batch rescore selects the k' best of those 512 lists with a radix select, and
+certifies against max(the (k'+1)-th score, the best 4th key) -- every row a workgroup left out
+scores at most its 4th.  A query that fails takes the second chance (every listed key above that
 bound, exactly rescored); one that fails again sends the batch through the thresholded path
 (sample pass, tau0, emit), whose own failures take the exact scan.
 
@@ -101,8 +101,8 @@ def test_top_path_off_switch(bsr_mod, oracle_mod, shard, monkeypatch):
 def test_top_path_near_duplicate_clusters(bsr_mod, oracle_mod, shard):
     """q0: 150 scattered near-duplicates -- the first pass's k' candidates are all duplicates, so
     it cannot certify; the second chance (every listed key above the wave bound) does.  q1: a run
-    of 300 consecutive near-duplicates -- spread over 300 waves by the strided rows, the same.
-    q2: 5000 scattered near-duplicates -- some wave holds more than 4, so its 4th key is a
+    of 300 consecutive near-duplicates -- spread over 150 workgroups by the strided pairs, the same.
+    q2: 5000 scattered near-duplicates -- some workgroup holds more than 4, so its 4th key is a
     duplicate and nothing certifies: the batch runs again on the thresholded path, whose
     overflowing list sends q2 to the exact scan.  Every result bit-exact."""
     ix, host, qh = shard
