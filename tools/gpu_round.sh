@@ -90,6 +90,16 @@ for step in $STEPS; do
     p50top)
       # round 6: the self-thresholded single-query path on / off, interleaved in one process
       run 400 "p50top" "$O/p50top.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200 ${P50MODES:-1,0}; cat "$O/p50top.txt" ;;
+    c4ab)
+      # round 6: the configs[3] bench (p50 over 10M rows) with the self-thresholded path on / off, interleaved
+      for r in 1 2; do
+        for v in 1 0; do
+          BSR_SKINNY_TOP=$v run 300 "c4 top=$v $r" "$O/c4ab_${v}_$r.json" python bench.py --config c4 --steps 5 --warmup 2 \
+              --verify 1 $NOB
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('top', sys.argv[2], d['p50_ms'], d.get('p50_kernels_ms_rank0'))" \
+              "$O/c4ab_${v}_$r.json" "$v"
+        done
+      done ;;
     toptests)
       # round 6: the new collective and single-query tests alone
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
