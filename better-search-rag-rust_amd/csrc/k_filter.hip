@@ -1389,18 +1389,24 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     // TOP: unit u holds eight strided pairs of rows, 2u, 2u + 1 of each eighth of the corpus
     // (A-row m = row (m >> 1) 2 n_units + 2u + (m & 1)), so a run of consecutive similar rows is
     // spread over consecutive units two at a time, i.e. over different workgroups: no workgroup's 4
-    // best come from one cluster of up to ~2 gridDim rows.  (Lab, p.top_layout: 0 = contiguous
-    // units as EMIT, no spread; 1 = sixteen strided rows; 3 = four strided quads.  p50 over 10M rows
-    // on one box, profiles/r06e_p50_top_layouts.txt: 1.2925 / 1.3092 / 1.3010 ms for layouts 0 / 1 /
-    // 2 against 1.3243 ms for the thresholded path.)
-    const uint32_t lay = TOP ? p.top_layout : 0u;
+    // best come from one cluster of up to ~2 gridDim rows.  (Lab, p.top_layout = 0: contiguous
+    // units as EMIT, no spread.  p50 over 10M rows on one box, profiles/r06e_p50_top_layouts.txt:
+    // 1.2925 / 1.3092 / 1.3010 ms for contiguous units / sixteen strided rows / strided pairs against
+    // 1.3243 ms for the thresholded path.)
+    const bool contig = !TOP || p.top_layout == 0;
     auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
-        if (!TOP || lay == 0) return u * 16 + m;
-        if (lay == 2) return (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
-        if (lay == 3) return (m >> 2) * (4 * n_units) + 4 * u + (m & 3);
-        return m * n_units + u;
+        return contig ? u * 16 + m : (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
     };
-    auto load = [&](i32x4_t (&fa)[NK], uint32_t u) {
+    // TOP: a lane's output rows 4h + i are two pairs, each in one 32-row scale block: their two
+    // scales are loaded with the unit's fragments (prefetched, as the fragments are)
+    auto load = [&](i32x4_t (&fa)[NK], float (&fs)[2], uint32_t u) {
+        if constexpr (TOP) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t rj = row_of(u, 4 * h + 2 * j);
+                fs[j] = p.a_scale[(rj < p.n_rows ? rj : p.n_rows - 1) / kQuantBlock];
+            }
+        }
         uint32_t r = row_of(u, q);
         r = r < p.n_rows ? r : p.n_rows - 1;  // tail rows: clamped, never emitted
         const uint8_t* a = p.A + (uint64_t)r * p.a_stride + h * 16;
@@ -1414,24 +1420,16 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
             }
     };
     float smax = -INFINITY;  // SAMPLE compact: running maximum of the 32-row block
-    auto process = [&](const i32x4_t (&fa)[NK], uint32_t u) {
+    auto process = [&](const i32x4_t (&fa)[NK], const float (&fs)[2], uint32_t u) {
         i32x4_acc_t acc = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < NK; ++s)
             if (s < (int)nk) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
         // register i: tile row u*16 + 4h + i, query q
         if constexpr (TOP) {
-            // the block scale of the row this lane loaded (A-row q), then of its output rows
-            // 4h + i, taken from the lanes that loaded them (lane 16h + 4h + i: same h, q = 4h + i;
-            // two distinct blocks per lane in the pair layout)
-            const uint32_t rq = row_of(u, q);
-            const float sc_own = p.a_scale[(rq < p.n_rows ? rq : p.n_rows - 1) / kQuantBlock];
             float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float sc = __shfl(sc_own, (int)(16 * h + 4 * h + i), kWave);
-                v[i] = ((float)acc[i] * sc) * sbq;
-            }
+            for (int i = 0; i < 4; ++i) v[i] = ((float)acc[i] * fs[i >> 1]) * sbq;
             const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
             // (strictly above the lane's 4th: a row at most its 4th stays within the bound; rare
             // once the lane holds 4 keys, ~4 ln(rows / 4) insertions)
@@ -1493,13 +1491,14 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     }
     if (n_my) {
         i32x4_t fa0[NK], fa1[NK];
-        load(fa0, unit_of(0));
+        float fs0[2] = {1.0f, 1.0f}, fs1[2] = {1.0f, 1.0f};
+        load(fa0, fs0, unit_of(0));
         for (uint32_t i = 0; i < n_my; i += 2) {
-            if (i + 1 < n_my) load(fa1, unit_of(i + 1));
-            process(fa0, unit_of(i));
+            if (i + 1 < n_my) load(fa1, fs1, unit_of(i + 1));
+            process(fa0, fs0, unit_of(i));
             if (i + 1 >= n_my) break;
-            if (i + 2 < n_my) load(fa0, unit_of(i + 2));
-            process(fa1, unit_of(i + 1));
+            if (i + 2 < n_my) load(fa0, fs0, unit_of(i + 2));
+            process(fa1, fs1, unit_of(i + 1));
         }
     }
     if constexpr (TOP) {

@@ -103,7 +103,7 @@ struct GemmArgs {
     // the batch's query count (padding queries keep no list)
     uint32_t* status;
     uint32_t n_q;
-    uint32_t top_layout;  // the skinny TOP row layout: 2 = the product (others: lab, k_filter.hip)
+    uint32_t top_layout;  // the skinny TOP row layout: 2 = the product strided pairs (0: lab, k_filter.hip)
 };
 // Dynamic tail of the emit filter: 1/kTailDiv of the row tiles; counters per (XCD pool, query
 // tile) (<= kTailCounters query tiles) after the per-query counters, cnt[qpad + x * n_qt + qt].
