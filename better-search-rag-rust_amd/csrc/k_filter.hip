@@ -1393,9 +1393,14 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     // units as EMIT, no spread.  p50 over 10M rows on one box, profiles/r06e_p50_top_layouts.txt:
     // 1.2925 / 1.3092 / 1.3010 ms for contiguous units / sixteen strided rows / strided pairs against
     // 1.3243 ms for the thresholded path.)
-    const bool contig = !TOP || p.top_layout == 0;
+    // (lab, p.top_layout = 3: 128-row blocks in 8-row stripes, A-row m of unit u = row
+    // 128 (u >> 3) + 8m + (u & 7): consecutive rows in consecutive units, a lane's four output rows
+    // in one scale block, and the units of a round within one window of the corpus)
+    const uint32_t lay = TOP ? p.top_layout : 0u;
     auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
-        return contig ? u * 16 + m : (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
+        if (lay == 0) return u * 16 + m;
+        if (lay == 3) return (u >> 3) * 128 + m * 8 + (u & 7);
+        return (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
     };
     // TOP: a lane's output rows 4h + i are two pairs, each in one 32-row scale block: their two
     // scales are loaded with the unit's fragments (prefetched, as the fragments are)
