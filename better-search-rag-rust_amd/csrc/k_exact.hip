@@ -1150,11 +1150,30 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     __shared__ uint64_t h_idx[kMergeMaxEntries], h_min[kMergeMaxEntries];
     const uint32_t q = blockIdx.x;
     const int lane = threadIdx.x;
+    // (the lambdas below read the kernel argument's fields through these locals: capturing the
+    // by-value argument itself makes it addressable, i.e. a copy in scratch -- 144 B per lane)
+    const auto m_cnt = a.cnt;
+    const auto m_force_hash = a.force_hash;
+    const auto m_cnt_stride = a.cnt_stride;
+    const auto m_dist_stride = a.dist_stride;
+    const auto m_excl = a.excl;
+    const auto m_excl_stride = a.excl_stride;
+    const auto m_fail_cnt = a.fail_cnt;
+    const auto m_fail_list = a.fail_list;
+    const auto m_first_nan = a.first_nan;
+    const auto m_hout_count = a.hout_count;
+    const auto m_hout_dist = a.hout_dist;
+    const auto m_hout_idx = a.hout_idx;
+    const auto m_idx_stride = a.idx_stride;
+    const auto m_need = a.need;
+    const auto m_st = a.st;
+    const auto m_st_all = a.st_all;
+    const auto m_st_stride = a.st_stride;
     float x_l = INFINITY;  // (certification) list `lane`'s exclusion bound for q
     auto merge_query = [&]() -> bool {
-        if (a.st_all && q == 0)  // every list's status words, compact
+        if (m_st_all && q == 0)  // every list's status words, compact
             for (uint32_t i = lane; i < P * kStWords; i += kWave)
-                a.st_all[i] = a.st[(uint64_t)(i / kStWords) * a.st_stride + i % kStWords];
+                m_st_all[i] = m_st[(uint64_t)(i / kStWords) * m_st_stride + i % kStWords];
         if (q >= nq) return false;
         // ONE batch of loads for the whole query (round 5: they were three dependent rounds --
         // counts, then each list's entries, then the certification bounds): every slot of every
@@ -1171,12 +1190,12 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             iv[u] = 0;
             if (u * kWave < (int)slots && f < slots) {
                 const uint32_t l = f / k_in, i = f - l * k_in;
-                dv[u] = dist[(uint64_t)l * a.dist_stride + (uint64_t)q * k_in + i];
-                iv[u] = idx[(uint64_t)l * a.idx_stride + (uint64_t)q * k_in + i];
+                dv[u] = dist[(uint64_t)l * m_dist_stride + (uint64_t)q * k_in + i];
+                iv[u] = idx[(uint64_t)l * m_idx_stride + (uint64_t)q * k_in + i];
             }
         }
-        const uint32_t c_l = lane < (int)P ? min(a.cnt[(uint64_t)lane * a.cnt_stride + q], k_in) : 0u;
-        x_l = (a.excl && lane < (int)P) ? a.excl[(uint64_t)lane * a.excl_stride + q] : INFINITY;
+        const uint32_t c_l = lane < (int)P ? min(m_cnt[(uint64_t)lane * m_cnt_stride + q], k_in) : 0u;
+        x_l = (m_excl && lane < (int)P) ? m_excl[(uint64_t)lane * m_excl_stride + q] : INFINITY;
         // list l's offset in the concatenation (exclusive prefix sum of the counts)
         uint32_t incl = c_l;
     #pragma unroll
@@ -1208,28 +1227,46 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
         auto put = [&](uint32_t p, uint64_t vi, float vd) {
             out_idx[(uint64_t)q * k + p] = vi;
             out_dist[(uint64_t)q * k + p] = vd;
-            if (a.hout_idx) {
-                host_put(a.hout_idx + (uint64_t)q * k + p, vi);
-                host_put(a.hout_dist + (uint64_t)q * k + p, vd);
+            if (m_hout_idx) {
+                host_put(m_hout_idx + (uint64_t)q * k + p, vi);
+                host_put(m_hout_dist + (uint64_t)q * k + p, vd);
             }
         };
         auto put_count = [&](uint32_t c) {
             out_count[q] = c;
-            if (a.hout_count) host_put(a.hout_count + q, c);
+            if (m_hout_count) host_put(m_hout_count + q, c);
         };
         if (__ballot(nan)) {
             if (lane == 0) {
                 put_count(0);
-                atomicMin(a.first_nan, q);
+                atomicMin(m_first_nan, q);
             }
             for (uint32_t p = lane; p < k; p += kWave) put(p, ~0ull, INFINITY);
             return true;
         }
+        // Lists whose index ranges are pairwise disjoint -- the rank shards of a parallel search --
+        // hold no index twice: no first-occurrence filter (round 6; the hash below is a chain of
+        // LDS atomics and two barriers).  Lane l < P: list l's [min, max] index.
+        uint64_t lo = ~0ull, hi = 0;
+        if (lane < (int)P)
+            for (uint32_t i = 0; i < c_l; ++i) {
+                const uint64_t x = s_idx[off_l + i];
+                lo = x < lo ? x : lo;
+                hi = x > hi ? x : hi;
+            }
+        bool ovl = false;
+        for (uint32_t m = 0; m < P; ++m) {
+            const uint64_t lo_m = shfl64(lo, (int)m), hi_m = shfl64(hi, (int)m);
+            const uint32_t c_m = (uint32_t)__shfl((int)c_l, (int)m, kWave);
+            ovl |= lane < (int)P && (uint32_t)lane != m && c_l && c_m && !(hi < lo_m || hi_m < lo);
+        }
+        const bool disjoint = __ballot(ovl) == 0 && !m_force_hash;
         // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
         // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
         // hash's empty mark, takes the pairwise check instead.)
         bool has_empty_mark = false;
-        for (uint32_t j = lane; j < total; j += kWave) has_empty_mark |= s_idx[j] == ~0ull;
+        if (!disjoint)
+            for (uint32_t j = lane; j < total; j += kWave) has_empty_mark |= s_idx[j] == ~0ull;
         const bool pairwise = __ballot(has_empty_mark) != 0;
         uint32_t hmask = 127;
         while (hmask + 1 < 2 * total && hmask + 1 < kMergeMaxEntries) hmask = 2 * hmask + 1;  // load <= 1
@@ -1237,7 +1274,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             uint64_t h = x * 0x9E3779B97F4A7C15ull;
             return (uint32_t)(h >> 40) & hmask;
         };
-        if (!pairwise) {
+        if (!disjoint && !pairwise) {
             for (uint32_t i = lane; i <= hmask; i += kWave) {
                 h_idx[i] = ~0ull;
                 h_min[i] = ~0ull;
@@ -1265,7 +1302,9 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             if (j < total) {
                 key = s_key[j];
                 const uint64_t x = s_idx[j];
-                if (!pairwise) {
+                if (disjoint) {
+                    // (every entry is its index's only one)
+                } else if (!pairwise) {
                     uint32_t sl = slot0(x);
                     while (h_idx[sl] != x) sl = (sl + 1) & hmask;
                     if (h_min[sl] != key) key = kKeyNone;
@@ -1288,28 +1327,28 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             }
         }
         if (lane == 0) put_count(got);
-        const uint64_t kth = (a.excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
+        const uint64_t kth = (m_excl && got == k) ? L.at((int)k - 1) : kKeyNone;  // (wave-uniform)
         // the smallest bound over the lists (NaN: nothing certifiable), loaded with the lists
         float xmin = x_l == x_l ? x_l : -INFINITY;
     #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) xmin = fminf(xmin, __shfl_xor(xmin, off, kWave));
         bool shared = false;
-        if (a.excl && lane == 0) {
+        if (m_excl && lane == 0) {
             // Certification of a global-threshold parallel search: every row left
             // out on rank l lies at a distance >= excl_l[q] (its kernel's bound, rounded down), so
             // the merged list is the reference's iff it holds need = min(k, corpus rows) entries and
             // its k-th distance lies strictly below every rank's bound (a shorter list only when
             // every row of the corpus was a candidate: every bound +inf).
-            bool ok = got >= a.need;
+            bool ok = got >= m_need;
             if (ok && got == k) {
                 ok = (double)s_dist[(uint32_t)kth] < (double)xmin;
             } else if (ok) {
                 ok = xmin == INFINITY;
             }
-            if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
+            if (!ok) m_fail_list[atomicAdd(m_fail_cnt, 1u)] = q;
             shared = !ok;
         }
-        return __shfl((int)shared, 0, kWave) != 0 || (a.st_all && q == 0);
+        return __shfl((int)shared, 0, kWave) != 0 || (m_st_all && q == 0);
     };
     // (publish) whether this wave wrote state the publishing workgroup reads: the status words
     // (q = 0), a failure entry, the lowest NaN query
@@ -1529,7 +1568,12 @@ hipError_t launch_merge_lists(const uint64_t* idx, const float* dist, const uint
     a.first_nan = first_nan;
     return launch_merge(a, s);
 }
-hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
+hipError_t launch_merge(const MergeArgs& a_in, hipStream_t s) {
+    MergeArgs a = a_in;
+    {  // (lab A/B: BSR_MERGE_HASH=1 keeps the first-occurrence filter for disjoint lists too)
+        const char* v = getenv("BSR_MERGE_HASH");
+        a.force_hash = v && v[0] == '1' ? 1u : 0u;
+    }
     const uint32_t P = a.P, nq = a.nq, k_in = a.k_in, k = a.k;
     if (P > (uint32_t)kWave || (uint64_t)P * k_in > kMergeMaxEntries || k > 4 * kWave) return hipErrorInvalidValue;
     const uint32_t e = (k + 63) / 64;

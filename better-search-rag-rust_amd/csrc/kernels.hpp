@@ -301,6 +301,7 @@ struct MergeArgs {
     size_t pub_bytes;
     uint32_t* pub_flag;
     uint32_t* pub_ticket;
+    uint32_t force_hash;  // (lab, set by launch_merge from BSR_MERGE_HASH) no disjoint-lists shortcut
 };
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
 // Keys -> (global index, distance) rows; also zeroes `status`, the status words of the

@@ -100,6 +100,17 @@ for step in $STEPS; do
               "$O/c4ab_${v}_$r.json" "$v"
         done
       done ;;
+    mergeab)
+      # round 6: the loopback step (rank 0 of 8, replaying $O/loop8.npz from looprec) with the merge's
+      # first-occurrence filter forced (BSR_MERGE_HASH=1) or skipped for disjoint rank lists, interleaved
+      for r in 1 2; do
+        for v in 0 1; do
+          BSR_MERGE_HASH=$v run 300 "mergeab hash=$v $r" "$O/mergeab_${v}_$r.json" python bench.py --comm loopback --gpus 8 \
+              --replay "$O/loop8.npz" --steps 100 --warmup 5 --verify 1 --no-cpu-baseline
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('hash', sys.argv[2], d['ms_per_step'], d['loopback']['missed_allgathers'])" \
+              "$O/mergeab_${v}_$r.json" "$v"
+        done
+      done ;;
     toptests)
       # round 6: the new collective and single-query tests alone
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
