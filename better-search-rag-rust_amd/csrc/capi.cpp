@@ -967,6 +967,7 @@ static int parallel_gtau(bsr_comm* c, bsr_index* ix, const float* queries, uint3
     }
     ma.pub_flag = c->h_flag_dev;
     ma.pub_ticket = c->pub_ticket.as<uint32_t>();
+    ma.lists_unique = 1;  // (each rank's list: its own search's top-k)
     BSR_HIP(launch_merge(ma, s));
     uint8_t* hm = c->h_mres;
     {

@@ -1154,6 +1154,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
     // by-value argument itself makes it addressable, i.e. a copy in scratch -- 144 B per lane)
     const auto m_cnt = a.cnt;
     const auto m_force_hash = a.force_hash;
+    const auto m_lists_unique = a.lists_unique;
     const auto m_cnt_stride = a.cnt_stride;
     const auto m_dist_stride = a.dist_stride;
     const auto m_excl = a.excl;
@@ -1244,9 +1245,10 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             for (uint32_t p = lane; p < k; p += kWave) put(p, ~0ull, INFINITY);
             return true;
         }
-        // Lists whose index ranges are pairwise disjoint -- the rank shards of a parallel search --
-        // hold no index twice: no first-occurrence filter (round 6; the hash below is a chain of
-        // LDS atomics and two barriers).  Lane l < P: list l's [min, max] index.
+        // Lists without repeats (lists_unique: each one rank's own top-k) whose index ranges are
+        // pairwise disjoint -- the rank shards of a parallel search -- hold no index twice: no
+        // first-occurrence filter (round 6; the hash below is a chain of LDS atomics and two
+        // barriers).  Lane l < P: list l's [min, max] index.
         uint64_t lo = ~0ull, hi = 0;
         if (lane < (int)P)
             for (uint32_t i = 0; i < c_l; ++i) {
@@ -1260,7 +1262,7 @@ __global__ __launch_bounds__(64) void k_merge_lists(MergeArgs a) {
             const uint32_t c_m = (uint32_t)__shfl((int)c_l, (int)m, kWave);
             ovl |= lane < (int)P && (uint32_t)lane != m && c_l && c_m && !(hi < lo_m || hi_m < lo);
         }
-        const bool disjoint = __ballot(ovl) == 0 && !m_force_hash;
+        const bool disjoint = m_lists_unique && !m_force_hash && __ballot(ovl) == 0;
         // First occurrences: an LDS hash of index -> smallest key (open addressing, 64-bit CAS
         // and min); an entry is kept iff its key is its index's minimum.  (An index of ~0, the
         // hash's empty mark, takes the pairwise check instead.)

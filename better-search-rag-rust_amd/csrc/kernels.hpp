@@ -302,6 +302,9 @@ struct MergeArgs {
     uint32_t* pub_flag;
     uint32_t* pub_ticket;
     uint32_t force_hash;  // (lab, set by launch_merge from BSR_MERGE_HASH) no disjoint-lists shortcut
+    // every list is one search's own top-k (no index twice within a list): lists whose index ranges
+    // are pairwise disjoint then skip the first-occurrence filter
+    uint32_t lists_unique;
 };
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
 // Keys -> (global index, distance) rows; also zeroes `status`, the status words of the
