@@ -521,7 +521,7 @@ static int emit_pass(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k) {
 // the skinny TOP row layout: 2, the strided pairs (BSR_TOP_LAYOUT=0: contiguous units, lab A/B only)
 static uint32_t top_layout_lab() {
     const char* lay = getenv("BSR_TOP_LAYOUT");
-    return lay && (lay[0] == '0' || lay[0] == '3') ? (uint32_t)(lay[0] - '0') : 2u;
+    return lay && lay[0] == '0' ? 0u : 2u;
 }
 
 // The self-thresholded filter pass: every wave's 4 best keys per query (launch_filter_skinny_top).

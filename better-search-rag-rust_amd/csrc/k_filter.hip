@@ -1389,18 +1389,17 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
     // TOP: unit u holds eight strided pairs of rows, 2u, 2u + 1 of each eighth of the corpus
     // (A-row m = row (m >> 1) 2 n_units + 2u + (m & 1)), so a run of consecutive similar rows is
     // spread over consecutive units two at a time, i.e. over different workgroups: no workgroup's 4
-    // best come from one cluster of up to ~2 gridDim rows.  (Lab, p.top_layout = 0: contiguous
-    // units as EMIT, no spread.  p50 over 10M rows on one box, profiles/r06e_p50_top_layouts.txt:
-    // 1.2925 / 1.3092 / 1.3010 ms for contiguous units / sixteen strided rows / strided pairs against
-    // 1.3243 ms for the thresholded path.)
-    // (lab, p.top_layout = 3: 128-row blocks in 8-row stripes, A-row m of unit u = row
-    // 128 (u >> 3) + 8m + (u & 7): consecutive rows in consecutive units, a lane's four output rows
-    // in one scale block, and the units of a round within one window of the corpus)
-    const uint32_t lay = TOP ? p.top_layout : 0u;
+    // best come from one cluster of up to ~2 gridDim rows.  The spread costs HBM efficiency: the
+    // rows of one load instruction sit in 8 places instead of one 12 KB stretch.  p50 over 10M rows,
+    // one process, interleaved (profiles/r06e_p50_top_layouts.txt, r06j_p50_top_layouts.txt):
+    // contiguous units as EMIT (lab, p.top_layout = 0) 1.2925 / 1.2944 ms, sixteen strided rows
+    // 1.3092, strided pairs 1.3010 / 1.3328, 128-row blocks in 8-row stripes 1.3702, against the
+    // thresholded path's 1.3243 / 1.3415.  Contiguous units are fastest, but a run of >= 4 of a
+    // query's top rows in one 16-row unit (consecutive chunks of one document) fills a list and
+    // sends the batch to the thresholded path: the pairs are kept.
+    const bool contig = !TOP || p.top_layout == 0;
     auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
-        if (lay == 0) return u * 16 + m;
-        if (lay == 3) return (u >> 3) * 128 + m * 8 + (u & 7);
-        return (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
+        return contig ? u * 16 + m : (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
     };
     // TOP: a lane's output rows 4h + i are two pairs, each in one 32-row scale block: their two
     // scales are loaded with the unit's fragments (prefetched, as the fragments are)
