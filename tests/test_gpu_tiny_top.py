@@ -135,3 +135,32 @@ def test_top_path_zero_query_takes_exact_scan(bsr_mod, oracle_mod, shard):
     st = ix.last_stats()
     _same(got, want, "zero query")
     assert st.n_exact_direct == 1, st.n_exact_direct
+
+
+@pytest.mark.parametrize("dim,nq,k", [(256, 3, 10), (200, 1, 5)])
+def test_top_path_other_widths(bsr_mod, oracle_mod, gpu, dim, nq, k):
+    """The self-thresholded path on rows of other widths (4 K slices: k_filter_skinny2<kSkTop, 4>;
+    200: a partial last slice and a zero-padded row tail), over 2.2M rows, with a planted
+    self-match in the last partial unit: bit-exact against the oracle, twice (graph replay)."""
+    import torch
+    n = 2_200_003
+    rows = torch.empty((n, dim), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(rows.data_ptr(), 0, n, dim, 9)
+    q = torch.empty((nq, dim), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(q.data_ptr(), 0, nq, dim, 10)
+    q[0] = rows[n - 1]
+    torch.cuda.synchronize()
+    ix = bsr_mod.Index(dim, max_k=64, device=0)
+    ix.load(rows)
+    host, qh = rows.cpu().numpy(), q.cpu().numpy()
+    del rows
+    torch.cuda.empty_cache()
+    want = oracle_mod.parallel_top_k(host, qh, k, size=THREADS, threads=THREADS)
+    for rep in range(3):
+        got = ix.local_top_k(qh, k)
+        st = ix.last_stats()
+        assert st.search_path & bsr_mod.BSR_PATH_SKINNY_TOP, st.search_path
+        assert st.n_fallback == 0
+        _same(got, want, f"dim {dim} nq {nq} k {k} rep {rep}")
+    assert got[0][0, 0] == n - 1 and got[1][0, 0] == 0.0
+    ix.close()
