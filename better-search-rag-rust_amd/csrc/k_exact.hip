@@ -808,7 +808,11 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     if ((uint32_t)(w * 64 + lane) < ld) ldq[w * 64 + lane] = a.qf32[(uint64_t)q * ld + w * 64 + lane];
     if (a.top_w) {
         // (LDS scratch for the heads and candidates: the product stage, first written after this)
-        if (w == 0) top_select(a, q, lsel, s_c, s_tx, s_ov, lane, reinterpret_cast<uint64_t*>(stage));
+        if (w == 0) {
+            BSR_STAMP(1, 5);  // (lab: no separate key arrival on this path)
+            top_select(a, q, lsel, s_c, s_tx, s_ov, lane, reinterpret_cast<uint64_t*>(stage));
+            BSR_STAMP(1, 1);
+        }
     } else if (w == 0) {
         constexpr int NR = 16;
         uint64_t xk[NR];

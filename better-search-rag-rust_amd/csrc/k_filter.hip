@@ -1941,11 +1941,13 @@ hipError_t launch_select_tau(const float* S, uint32_t s_ld, uint32_t n_s, uint32
                              const uint32_t* qflags, uint32_t ks, float* tau, uint32_t* cnt, uint32_t* status,
                              hipStream_t s, uint64_t* smax) {
     if (ks > 2 * kWave) return hipErrorInvalidValue;
-    static const bool m_on = [] {  // (BSR_SELECT_TAU_M=0: the 4-wave kernel instead, for A/B runs)
+    // (BSR_SELECT_TAU_M=0: the 4-wave kernel instead; =2 (lab): the 16-wave kernel for every batch
+    // size, for A/B runs)
+    static const int m_on = [] {
         const char* v = getenv("BSR_SELECT_TAU_M");
-        return !(v && v[0] == '0');
+        return v && v[0] == '0' ? 0 : v && v[0] == '2' ? 2 : 1;
     }();
-    if (m_on && ks <= kWave && qpad <= 16 && n_s > 32 * kWave && n_s <= 16 * 16 * kWave)
+    if (m_on && ks <= kWave && (qpad <= 16 || m_on == 2) && n_s > 32 * kWave && n_s <= 16 * 16 * kWave)
         hipLaunchKernelGGL(k_select_tau_m<16>, dim3(qpad), dim3(1024), 0, s, S, s_ld, n_s, nq, qpad, qflags, ks,
                            tau, cnt, status, smax);
     else if (ks <= kWave && n_s <= 32 * kWave && qpad % 4 == 0)

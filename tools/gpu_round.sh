@@ -39,7 +39,9 @@
 #   p50lib:A,B  p50 of one query over 10M rows per libbsr build, interleaved
 #   p50rs       the single-query rescore events (tools/diag/p50_rescore.py), kp on / off
 #   p50st       the tiny-batch rescore's lab stamps + a kernel timeline of single-query searches at 2M rows
+#               (P50ROWS=10000000: the self-thresholded path)
 #   seltau      tools/microbench/seltau_ab: k_select_tau_m vs k_select_tau, bit for bit
+#   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
 #   abflat      the loopback step with the dealt-rows global-threshold rescore on / off (after looprec)
@@ -131,11 +133,11 @@ for step in $STEPS; do
       cat "$O/p50rs.txt" ;;
     p50st)
       # the single query's rescore phases (lab stamps) and its kernel timeline (rocprof trace)
-      BSR_LIB=tools/ab/libbsr_stamps.so BSR_READ_STAMPS=1 timeout -k 10 200 python3 tools/diag/p50_rescore.py 2000000 1 \
+      BSR_LIB=tools/ab/libbsr_stamps.so BSR_READ_STAMPS=1 timeout -k 10 200 python3 tools/diag/p50_rescore.py ${P50ROWS:-2000000} 1 \
           > "$O/p50_stamps.txt" 2>> "$O/err.txt" || exit 1
       cat "$O/p50_stamps.txt"
       run 300 "p50 trace" "$O/p50_trace.txt" rocprofv3 --kernel-trace --output-format csv -d "$O/tlp50" -o run -- \
-          python3 tools/diag/p50_rescore.py 2000000 1
+          python3 tools/diag/p50_rescore.py ${P50ROWS:-2000000} 1
       f=$(find "$O/tlp50" -name "*kernel_trace.csv" | head -1)
       python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_p50.txt"; tail -30 "$O/timeline_p50.txt" ;;
     p50lib:*)
@@ -189,6 +191,19 @@ for step in $STEPS; do
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
+    seltauab)
+      # tau0's selection at 10M x 1000 (9766 values per query): the 4-wave kernel (BSR_SELECT_TAU_M=1,
+      # the product) against the 16-wave kernel (=2), rocprof averages, two interleaved rounds;
+      # the spot check (--verify 2) confirms identical results
+      for r in 1 2; do
+        for v in 1 2; do
+          BSR_SELECT_TAU_M=$v run 300 "seltau $v round $r" "$O/seltau_${v}_$r.json" rocprofv3 --kernel-trace --stats \
+              --output-format csv -d "$O/seltau_${v}_$r" -o run -- python3 bench.py --steps 10 --warmup 3 --verify 2 $NOB
+          f=$(find "$O/seltau_${v}_$r" -name "*kernel_stats.csv" | head -1)
+          echo "M=$v round $r: $(grep -h -E 'k_select_tau|k_filter_qs16<false' "$f" | cut -d, -f1,2,4 | tr '\n' ' ')"
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('  q/s', d['value'], 'spot', d.get('parity_spot_check',{}).get('indices_equal'), d.get('parity_spot_check',{}).get('distance_bits_equal'))" "$O/seltau_${v}_$r.json"
+        done
+      done ;;
     prof)
       run 300 "rocprof stats" "$O/bench_prof.json" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
           python3 bench.py --steps 10 --warmup 3 --verify 0 $NOB
