@@ -283,7 +283,7 @@ for step in $STEPS; do
       python3 tools/diag/api_gap.py "$O/apiloop" > "$O/api_gap_loop8.txt"; cat "$O/api_gap_loop8.txt" ;;
     looptl)
       run 300 "loopback trace" "$O/bench_loop8_prof.json" rocprofv3 --kernel-trace --output-format csv -d "$O/tlloop" -o run -- \
-          python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 $NOB
+          python3 bench.py --comm loopback --gpus 8 --replay "$O/loop8.npz" --verify 0 --steps 30 --p50-iters 3 --settle-ms 0 $NOB
       f=$(find "$O/tlloop" -name "*kernel_trace.csv" | head -1)
       python3 tools/diag/timeline.py "$f" 40 > "$O/timeline_loop8.txt"; tail -30 "$O/timeline_loop8.txt" ;;
     mpub)
