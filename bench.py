@@ -594,6 +594,7 @@ def main():
         step(1, qdev[1:2].data_ptr())
         lat.append((time.perf_counter() - t1) * 1e3)
     p50 = statistics.median(lat) if lat else None
+    p50_path = index.last_stats().search_path  # (BSR_PATH_SKINNY_TOP: the self-thresholded filter)
     index.set_profile(2)
     index.profile(reset=True)
     for _ in range(max(3, min(args.p50_iters, 10))):
@@ -644,7 +645,8 @@ def main():
         if args.filter == "i8" and Q <= 16:
             # <= 16 queries on an int8 index: the skinny filter (HBM-bound)
             kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
-            kname = f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>"
+            kname = (f"k_filter_skinny2<{2 if st.search_path & bsr.BSR_PATH_SKINNY_TOP else 1}, {kv}>" if kv
+                     else "k_filter_skinny<true>")
             sbytes = n_local * nk * 64
             gbs = sbytes / (emit_ms * 1e-3) / 1e9 if emit_ms > 0 else None
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1) if gbs else None,
@@ -706,7 +708,9 @@ def main():
             },
             "p50_ms": round(p50, 4) if p50 is not None else None,
             "p50_config": f"1 query over {n_total} rows on {world} GPU(s)" + (
-                " (int8 skinny filter, HBM-bound, + exact rescore)" if args.filter == "i8" else
+                (" (int8 skinny filter keeping each workgroup's 4 best rows, HBM-bound, + exact rescore)"
+                 if p50_path & bsr.BSR_PATH_SKINNY_TOP else " (int8 skinny filter, HBM-bound, + exact rescore)")
+                if args.filter == "i8" else
                 " (exact f32 scan, HBM-bound)"),
             "roofline": roof,
             "local_search_ms_per_step": round(local_ms, 4),
@@ -747,7 +751,8 @@ def main():
         if kms > 0:
             if args.filter == "i8":
                 kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
-                kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<true, {kv}>" if kv else "k_filter_skinny<true>")
+                mode = 2 if p50_path & bsr.BSR_PATH_SKINNY_TOP else 1  # (kSkTop / kSkEmit)
+                kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<{mode}, {kv}>" if kv else "k_filter_skinny<true>")
             else:
                 kbytes, kn = n_local * nk * 64 * 4, "k_scan_exact<1,1>"
             gbs = kbytes / (kms * 1e-3) / 1e9
