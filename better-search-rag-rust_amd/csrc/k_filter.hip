@@ -1540,6 +1540,159 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------
+// Skinny filter, row modes, with the rows streamed into LDS by LDS-DMA (round 6, lab switch
+// BSR_SKINNY_GLDS=1; MI355X_MICROARCH.md 'ldsdma-fill', 'nt-weights': a once-read stream moved by
+// global_load_lds with the non-temporal policy reached 6.5-6.8 TB/s chip-wide against 6.4 for the
+// default policy).  The same rows, scores and keys as k_filter_skinny2 (EMIT / TOP): each wave keeps
+// a ring of SL units in LDS -- a unit's NK K slices (16 rows x 64 B each: lane (row q, piece h)
+// fetches exactly the 16 bytes its MFMA fragment needs, so a slice is read back with one
+// ds_read_b128 per lane) and the two block scales of the lane's rows -- and issues the DMA of unit
+// i + SL - 1 before it waits (counted vmcnt) for unit i.  Two waves per workgroup, so the workgroup
+// count -- TOP's list count -- is k_filter_skinny2's, at two workgroups per CU (LDS).  Only the B
+// fragments are ordinary loads, consumed before the stream starts (an ordinary load's use while
+// LDS-DMA is outstanding makes the compiler drain every DMA).
+// ------------------------------------------------------------------------------------
+#ifndef BSR_SKINNY_GLDS_AUX
+#define BSR_SKINNY_GLDS_AUX 2  // (nt)
+#endif
+template <int MODE, int NK>
+__global__ __launch_bounds__(128) void k_filter_skinny_glds(GemmArgs p) {
+    constexpr bool EMIT = MODE == kSkEmit, TOP = MODE == kSkTop;
+    static_assert(EMIT || TOP, "row modes only");
+    constexpr int NW = 2, SL = 3, SCB = 512, SLOT = NK * 1024 + SCB, PER = NK + 2;
+    __shared__ __attribute__((aligned(1024))) uint8_t ring[NW * SL * SLOT];
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t q = lane & 15, h = lane >> 4;
+    const uint32_t n_units = (p.n_rows + 15) / 16;
+    const uint32_t nwaves = gridDim.x * NW, wid = TOP ? w * gridDim.x + blockIdx.x : blockIdx.x * NW + w;
+    const float sbq = p.b_scale[q];
+    const float tauq = EMIT ? p.tau[q] : 0.0f;
+    i32x4_t fb[NK];
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+        fb[s] = *reinterpret_cast<const i32x4_t*>(p.B + (uint64_t)q * p.row_bytes + h * 16 + s * kSliceB);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    uint64_t tk[4] = {kKeyNone, kKeyNone, kKeyNone, kKeyNone};
+    float tk3 = -INFINITY;
+    const bool live = !TOP || q < p.n_q;
+    if (TOP && blockIdx.x == 0 && threadIdx.x < 16) {
+        p.cnt[threadIdx.x] = 4 * gridDim.x;
+        if (threadIdx.x == 0) { p.status[kStFail] = 0; p.status[kStEmitted] = 0; p.status[kStFail2] = 0; }
+    }
+    const bool contig = !TOP || p.top_layout == 0;
+    auto row_of = [&](uint32_t u, uint32_t m) -> uint32_t {
+        return contig ? u * 16 + m : (m >> 1) * (2 * n_units) + 2 * u + (m & 1);
+    };
+    const uint32_t n_rows = p.n_rows;
+    uint8_t* const wr = ring + w * (SL * SLOT);
+    const uint32_t n_my = wid < n_units ? (n_units - 1 - wid) / nwaves + 1 : 0;
+    auto issue = [&](uint32_t i) {
+        const uint32_t u = wid + i * nwaves;
+        uint8_t* const dst = wr + (i % SL) * SLOT;
+        uint32_t r = row_of(u, q);
+        r = r < n_rows ? r : n_rows - 1;  // tail rows: clamped, never emitted
+        const uint8_t* const src = p.A + (uint64_t)r * p.a_stride + h * 16;
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+            __builtin_amdgcn_global_load_lds((const void*)(src + s * kSliceB), (lds_void_t*)(dst + s * 1024), 16, 0,
+                                             BSR_SKINNY_GLDS_AUX);
+        // the block scales of the lane's output rows 4h .. 4h + 3 (TOP: two pairs; EMIT: the unit's)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            uint32_t rj = TOP ? row_of(u, 4 * h + 2 * j) : u * 16;
+            rj = rj < n_rows ? rj : n_rows - 1;
+            __builtin_amdgcn_global_load_lds((const void*)(p.a_scale + rj / kQuantBlock),
+                                             (lds_void_t*)(dst + NK * 1024 + j * 256), 4, 0, BSR_SKINNY_GLDS_AUX);
+        }
+    };
+    if (n_my) issue(0);
+    if (n_my > 1) issue(1);
+    for (uint32_t i = 0; i < n_my; ++i) {
+        const uint32_t u = wid + i * nwaves;
+        // unit i landed: the units issued after it stay in flight (PER DMAs each)
+        // (the builtin, not asm: the compiler's own wait counting sees it; vmcnt N: bits 3:0 and
+        // 15:14, expcnt and lgkmcnt left at their maxima)
+        constexpr int kW2 = ((2 * PER) & 15) | (((2 * PER) >> 4) << 14) | 0x0F70;
+        constexpr int kW1 = (PER & 15) | ((PER >> 4) << 14) | 0x0F70;
+        if (i + 2 < n_my) {
+            issue(i + 2);
+            __builtin_amdgcn_s_waitcnt(kW2);
+        } else if (i + 1 < n_my) {
+            __builtin_amdgcn_s_waitcnt(kW1);
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        const uint8_t* const src = wr + (i % SL) * SLOT;
+        i32x4_t fa[NK];
+#pragma unroll
+        for (int s = 0; s < NK; ++s) fa[s] = *reinterpret_cast<const i32x4_t*>(src + s * 1024 + lane * 16);
+        const float fs0 = reinterpret_cast<const float*>(src + NK * 1024)[lane];
+        const float fs1 = reinterpret_cast<const float*>(src + NK * 1024 + 256)[lane];
+        i32x4_acc_t acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < NK; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
+        // register i: row row_of(u, 4h + i), query q
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = ((float)acc[k] * (k < 2 ? fs0 : fs1)) * sbq;
+        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        if constexpr (TOP) {
+            if (live && mx > tk3) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t rw = row_of(u, 4 * h + k);
+                    if (v[k] > tk3 && rw < n_rows) {
+                        top4_insert(tk, score_key(v[k], rw));
+                        tk3 = tk[3] == kKeyNone ? -INFINITY : score_key_score(tk[3]);
+                    }
+                }
+            }
+        } else {
+            if (__ballot(mx >= tauq)) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t row = u * 16 + 4 * h + k;
+                    if (v[k] >= tauq && row < n_rows) {
+                        const uint32_t gp = atomicAdd(p.cnt + q, 1u);
+                        if (gp < p.cap) p.cand[(uint64_t)q * p.cap + gp] = score_key(v[k], row);
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (TOP) {
+        // as k_filter_skinny2: the query's four lanes merge, then wave 0 the workgroup's waves
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            uint64_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)tk[j], off, kWave);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(tk[j] >> 32), off, kWave);
+                o[j] = ((uint64_t)hi << 32) | lo;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) top4_insert(tk, o[j]);
+        }
+        __shared__ uint64_t wl[NW][16][4];
+        if (h == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wl[w][q][j] = tk[j];
+        __syncthreads();
+        if (w == 0 && h == 0) {
+#pragma unroll
+            for (int o = 1; o < NW; ++o)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) top4_insert(tk, wl[o][q][j]);
+            uint64_t* dst = p.cand + ((uint64_t)q * gridDim.x + blockIdx.x) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dst[j] = tk[j];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Threshold per query from the sample scores: tau0 = the ks-th largest value of S (sample
 // scores, or their maxima over 32 sampled rows -- never above the ks-th largest sample),
 // so that about ks * stride rows of the shard or more reach it.  4 waves per query.  Also
@@ -1865,9 +2018,20 @@ static uint32_t skinny2_grid(uint32_t n_rows) {
     return std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
 }
 uint32_t skinny_top_lists(uint32_t n_rows) { return skinny2_grid(n_rows); }
+// (lab, BSR_SKINNY_GLDS=1, read per launch: the row modes over 768-byte rows by LDS-DMA)
+bool skinny_glds_lab() {
+    const char* v = getenv("BSR_SKINNY_GLDS");
+    return v && v[0] == '1';
+}
 template <int MODE>
 static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB;
+    if constexpr (MODE != kSkSample) {
+        if (nk == 12 && skinny_glds_lab()) {
+            BSR_KLAUNCH((k_filter_skinny_glds<MODE, 12>), dim3(skinny2_grid(a.n_rows)), dim3(128), s, e0, e1, a);
+            return;
+        }
+    }
     const dim3 g(nk <= 16 ? skinny2_grid(a.n_rows) : skinny_grid(a.n_rows)), b(256);
     if (nk <= 4) BSR_KLAUNCH((k_filter_skinny2<MODE, 4>), g, b, s, e0, e1, a);
     else if (nk <= 8) BSR_KLAUNCH((k_filter_skinny2<MODE, 8>), g, b, s, e0, e1, a);

@@ -16,6 +16,19 @@ import torch  # noqa: E402,F401  (before libbsr: one HIP runtime per process)
 import bsr  # noqa: E402
 
 
+def set_mode(mode):
+    os.environ["BSR_SKINNY_TOP"] = mode[0]
+    base = mode.rstrip("g")
+    if ":" in base:
+        os.environ["BSR_TOP_LAYOUT"] = base.split(":")[1]
+    else:
+        os.environ.pop("BSR_TOP_LAYOUT", None)
+    if mode.endswith("g"):
+        os.environ["BSR_SKINNY_GLDS"] = "1"
+    else:
+        os.environ.pop("BSR_SKINNY_GLDS", None)
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
@@ -48,12 +61,9 @@ def main():
     modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["1", "0"]
     for r in range(rounds):
         for mode in modes:
-            # "0": the thresholded path; "1": the self-thresholded path; "1:L": with the lab row layout L
-            os.environ["BSR_SKINNY_TOP"] = mode[0]
-            if ":" in mode:
-                os.environ["BSR_TOP_LAYOUT"] = mode.split(":")[1]
-            else:
-                os.environ.pop("BSR_TOP_LAYOUT", None)
+            # "0": the thresholded path; "1": the self-thresholded path; "1:L": with the lab row layout L;
+            # a trailing "g": the lab LDS-DMA skinny filter (BSR_SKINNY_GLDS=1)
+            set_mode(mode)
             for _ in range(20):
                 one(1)
             lat = []
@@ -76,11 +86,7 @@ def main():
     print(f"results of the {len(modes)} paths over 8 queries: {'IDENTICAL' if same else 'DIFFER'}", flush=True)
     # kernel times per mode (profile level 1: the filter events; level 2 every stage)
     for mode in modes:
-        os.environ["BSR_SKINNY_TOP"] = mode[0]
-        if ":" in mode:
-            os.environ["BSR_TOP_LAYOUT"] = mode.split(":")[1]
-        else:
-            os.environ.pop("BSR_TOP_LAYOUT", None)
+        set_mode(mode)
         ix.set_profile(2)
         ix.profile(reset=True)
         for _ in range(20):
