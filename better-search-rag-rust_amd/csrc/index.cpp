@@ -780,8 +780,8 @@ int bsr_index::search_device(const float* queries, uint32_t nq, uint32_t k, int 
     if (top) stats.search_path |= BSR_PATH_SKINNY_TOP;
     const bool graphable = use_filter && n > 0 && (!profiling(ix) || prof_level == 0) && !force_threshold;
     SearchGraph& gs = graphs[cur];
-    // (the graph key: the TOP row layout and the lab LDS-DMA skinny filter, both read per search)
-    const uint32_t lay = (top ? top_layout_lab() : 2u) | (skinny_glds_lab() ? 0x100u : 0u);
+    // (the graph key: the TOP row layout and the skinny filter's A/B switch, both read per search)
+    const uint32_t lay = (top ? top_layout_lab() : 2u) | (skinny_glds_on() ? 0x100u : 0u);
     const bool same_shape = warm.nq == nq && warm.k == k && warm.qsrc == qsrc && warm.n == n &&
                             warm.timed == (profiling(ix) ? prof_level : 0) && warm.top == top &&
                             warm.top_layout == lay;

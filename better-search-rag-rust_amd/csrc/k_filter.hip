@@ -1540,20 +1540,25 @@ __global__ __launch_bounds__(256) void k_filter_skinny2(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------
-// Skinny filter, row modes, with the rows streamed into LDS by LDS-DMA (round 6, lab switch
-// BSR_SKINNY_GLDS=1; MI355X_MICROARCH.md 'ldsdma-fill', 'nt-weights': a once-read stream moved by
-// global_load_lds with the non-temporal policy reached 6.5-6.8 TB/s chip-wide against 6.4 for the
-// default policy).  The same rows, scores and keys as k_filter_skinny2 (EMIT / TOP): each wave keeps
-// a ring of SL units in LDS -- a unit's NK K slices (16 rows x 64 B each: lane (row q, piece h)
-// fetches exactly the 16 bytes its MFMA fragment needs, so a slice is read back with one
-// ds_read_b128 per lane) and the two block scales of the lane's rows -- and issues the DMA of unit
-// i + SL - 1 before it waits (counted vmcnt) for unit i.  Two waves per workgroup, so the workgroup
-// count -- TOP's list count -- is k_filter_skinny2's, at two workgroups per CU (LDS).  Only the B
-// fragments are ordinary loads, consumed before the stream starts (an ordinary load's use while
-// LDS-DMA is outstanding makes the compiler drain every DMA).
+// Skinny filter, row modes, with the rows streamed into LDS by LDS-DMA (round 6; the product for
+// 768-byte rows).  The same rows, scores and keys as k_filter_skinny2 (EMIT / TOP): each wave keeps a
+// ring of SL units in LDS -- a unit's NK K slices (16 rows x 64 B each: lane (row q, piece h) fetches
+// exactly the 16 bytes its MFMA fragment needs, so a slice is read back with one ds_read_b128 per
+// lane) and the two block scales of the lane's rows -- and refills a unit's slot as soon as its
+// fragments are in registers, so SL units stay in flight through the MFMAs and the epilogue.  Two
+// waves per workgroup, so the workgroup count -- TOP's list count -- is k_filter_skinny2's, at two
+// workgroups per CU (LDS).  Only the B fragments are ordinary loads, consumed before the stream
+// starts (an ordinary load's use while LDS-DMA is outstanding makes the compiler drain every DMA).
+// One query over 10M rows, one process, interleaved against k_filter_skinny2 (BSR_SKINNY_GLDS=0;
+// profiles/r06q_p50glds_*.txt, r06r_*): the self-thresholded path 1.3125 / 1.3143 vs 1.3318 / 1.3310
+// ms p50 (filter 1.260 / 1.263 vs 1.279 / 1.280), the thresholded path 1.318 vs 1.340, and 0.2342
+// vs 0.2385 ms at the 1.25M-row rank shard.  Two units in flight instead of three: the same.  The
+// non-temporal policy (MI355X_MICROARCH.md 'nt-weights', aux = 2) made the filter 16% slower here
+// (r06o_*): these rows are not a once-read weight stream the guide measured, each 16-row load
+// touching sixteen half lines.
 // ------------------------------------------------------------------------------------
 #ifndef BSR_SKINNY_GLDS_AUX
-#define BSR_SKINNY_GLDS_AUX 2  // (nt)
+#define BSR_SKINNY_GLDS_AUX 0  // (the default policy; 2 = nt: +16% filter time, profiles/r06o_*)
 #endif
 template <int MODE, int NK>
 __global__ __launch_bounds__(128) void k_filter_skinny_glds(GemmArgs p) {
@@ -1606,29 +1611,33 @@ __global__ __launch_bounds__(128) void k_filter_skinny_glds(GemmArgs p) {
                                              (lds_void_t*)(dst + NK * 1024 + j * 256), 4, 0, BSR_SKINNY_GLDS_AUX);
         }
     };
-    if (n_my) issue(0);
-    if (n_my > 1) issue(1);
+    // SL units in flight: unit i + SL is issued into unit i's slot as soon as unit i's fragments
+    // and scales are in registers, so the stream keeps SL units in flight through the MFMAs and
+    // the epilogue
+#pragma unroll
+    for (uint32_t j = 0; j < (uint32_t)SL; ++j)
+        if (j < n_my) issue(j);
     for (uint32_t i = 0; i < n_my; ++i) {
         const uint32_t u = wid + i * nwaves;
-        // unit i landed: the units issued after it stay in flight (PER DMAs each)
+        // unit i landed: the units issued after it (at most SL - 1) stay in flight, PER DMAs each
         // (the builtin, not asm: the compiler's own wait counting sees it; vmcnt N: bits 3:0 and
         // 15:14, expcnt and lgkmcnt left at their maxima)
         constexpr int kW2 = ((2 * PER) & 15) | (((2 * PER) >> 4) << 14) | 0x0F70;
         constexpr int kW1 = (PER & 15) | ((PER >> 4) << 14) | 0x0F70;
-        if (i + 2 < n_my) {
-            issue(i + 2);
-            __builtin_amdgcn_s_waitcnt(kW2);
-        } else if (i + 1 < n_my) {
-            __builtin_amdgcn_s_waitcnt(kW1);
-        } else {
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-        }
+        static_assert(SL == 3, "the waits below count two younger units");
+        if (i + 2 < n_my) __builtin_amdgcn_s_waitcnt(kW2);
+        else if (i + 1 < n_my) __builtin_amdgcn_s_waitcnt(kW1);
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
         const uint8_t* const src = wr + (i % SL) * SLOT;
         i32x4_t fa[NK];
 #pragma unroll
         for (int s = 0; s < NK; ++s) fa[s] = *reinterpret_cast<const i32x4_t*>(src + s * 1024 + lane * 16);
         const float fs0 = reinterpret_cast<const float*>(src + NK * 1024)[lane];
         const float fs1 = reinterpret_cast<const float*>(src + NK * 1024 + 256)[lane];
+        // (every read of the slot complete -- lgkmcnt(0), vmcnt and expcnt at their maxima --
+        // before the DMA that refills it)
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (i + SL < n_my) issue(i + SL);
         i32x4_acc_t acc = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < NK; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s], fb[s], acc, 0, 0, 0);
@@ -2018,16 +2027,17 @@ static uint32_t skinny2_grid(uint32_t n_rows) {
     return std::min<uint32_t>(512, std::max<uint32_t>(1, (units + 3) / 4));
 }
 uint32_t skinny_top_lists(uint32_t n_rows) { return skinny2_grid(n_rows); }
-// (lab, BSR_SKINNY_GLDS=1, read per launch: the row modes over 768-byte rows by LDS-DMA)
-bool skinny_glds_lab() {
+// The row modes over 768-byte rows take k_filter_skinny_glds (BSR_SKINNY_GLDS=0, read per launch:
+// k_filter_skinny2 instead, for A/B runs)
+bool skinny_glds_on() {
     const char* v = getenv("BSR_SKINNY_GLDS");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
 }
 template <int MODE>
 static void launch_skinny(const GemmArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const uint32_t nk = a.row_bytes / kSliceB;
     if constexpr (MODE != kSkSample) {
-        if (nk == 12 && skinny_glds_lab()) {
+        if (nk == 12 && skinny_glds_on()) {
             BSR_KLAUNCH((k_filter_skinny_glds<MODE, 12>), dim3(skinny2_grid(a.n_rows)), dim3(128), s, e0, e1, a);
             return;
         }

@@ -135,7 +135,7 @@ hipError_t launch_filter_skinny_emit(const GemmArgs& a, hipStream_t s, hipEvent_
 // cnt[q] = 4 W for q < 16; the status words kStFail / kStEmitted / kStFail2 are zeroed.
 hipError_t launch_filter_skinny_top(const GemmArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 uint32_t skinny_top_lists(uint32_t n_rows);
-bool skinny_glds_lab();  // (lab: BSR_SKINNY_GLDS=1, the LDS-DMA skinny filter; read per call)
+bool skinny_glds_on();  // the LDS-DMA skinny filter for 768-byte rows (BSR_SKINNY_GLDS=0: off; read per call)
 // Shards of at least this many rows take the self-thresholded path for batches of <= 16 queries
 // and k' <= 63 (every wave of the 512-workgroup grid then holds >= 64 units of 16 rows).
 constexpr uint64_t kSkinnyTopMinRows = 2u << 20;

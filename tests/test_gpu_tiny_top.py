@@ -98,6 +98,23 @@ def test_top_path_off_switch(bsr_mod, oracle_mod, shard, monkeypatch):
     _same(got, want, "self-thresholded")
 
 
+@pytest.mark.parametrize("top", ["1", "0"])
+def test_skinny_filter_kernels_agree(bsr_mod, oracle_mod, shard, monkeypatch, top):
+    """768-byte rows take the LDS-DMA skinny filter (k_filter_skinny_glds); BSR_SKINNY_GLDS=0 runs
+    k_filter_skinny2 instead -- both row modes (self-thresholded, thresholded), the same bits, the
+    planted clusters included (their second chance and rerun)."""
+    ix, host, qh = shard
+    qs = np.ascontiguousarray(qh[[0, 1, 3, 5, 6, 11]])
+    want = _oracle(oracle_mod, host, qs, 10)
+    monkeypatch.setenv("BSR_SKINNY_TOP", top)
+    for glds in ("1", "0", "1"):
+        monkeypatch.setenv("BSR_SKINNY_GLDS", glds)
+        for rep in range(2):
+            got = ix.local_top_k(qs, 10)
+            assert bool(ix.last_stats().search_path & bsr_mod.BSR_PATH_SKINNY_TOP) == (top == "1")
+            _same(got, want, f"top={top} glds={glds} rep {rep}")
+
+
 def test_top_path_near_duplicate_clusters(bsr_mod, oracle_mod, shard):
     """q0: 150 scattered near-duplicates -- the first pass's k' candidates are all duplicates, so
     it cannot certify; the second chance (every listed key above the wave bound) does.  q1: a run

@@ -23,10 +23,7 @@ def set_mode(mode):
         os.environ["BSR_TOP_LAYOUT"] = base.split(":")[1]
     else:
         os.environ.pop("BSR_TOP_LAYOUT", None)
-    if mode.endswith("g"):
-        os.environ["BSR_SKINNY_GLDS"] = "1"
-    else:
-        os.environ.pop("BSR_SKINNY_GLDS", None)
+    os.environ["BSR_SKINNY_GLDS"] = "1" if mode.endswith("g") else "0"
 
 
 def main():
@@ -62,7 +59,7 @@ def main():
     for r in range(rounds):
         for mode in modes:
             # "0": the thresholded path; "1": the self-thresholded path; "1:L": with the lab row layout L;
-            # a trailing "g": the lab LDS-DMA skinny filter (BSR_SKINNY_GLDS=1)
+            # a trailing "g": the LDS-DMA skinny filter (BSR_SKINNY_GLDS=1; without it: =0, k_filter_skinny2)
             set_mode(mode)
             for _ in range(20):
                 one(1)

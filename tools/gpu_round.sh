@@ -41,8 +41,9 @@
 #   p50st       the tiny-batch rescore's lab stamps + a kernel timeline of single-query searches at 2M rows
 #               (P50ROWS=10000000: the self-thresholded path)
 #   seltau      tools/microbench/seltau_ab: k_select_tau_m vs k_select_tau, bit for bit
-#   gldstests   the single-query / small-batch tests with the lab LDS-DMA skinny filter (BSR_SKINNY_GLDS=1)
-#   p50glds     p50 A/B of the lab LDS-DMA skinny filter at 10M (self-thresholded) and 1.25M (thresholded)
+#   gldstests   the single-query / small-batch tests with k_filter_skinny2 at 768-wide rows (BSR_SKINNY_GLDS=0)
+#   p50glds     p50 A/B of the LDS-DMA skinny filter against k_filter_skinny2 at 10M (self-thresholded and
+#               thresholded) and 1.25M (thresholded)
 #   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
@@ -95,14 +96,19 @@ for step in $STEPS; do
       # round 6: the self-thresholded single-query path on / off, interleaved in one process
       run 400 "p50top" "$O/p50top.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200 ${P50MODES:-1,0}; cat "$O/p50top.txt" ;;
     p50glds)
-      # round 6 (lab): the LDS-DMA skinny filter (BSR_SKINNY_GLDS=1) against the product, interleaved:
+      # round 6: the LDS-DMA skinny filter (BSR_SKINNY_GLDS=1) against k_filter_skinny2 (=0), interleaved:
       # the self-thresholded path at 10M rows and the thresholded path at the 1.25M-row rank shard
       run 400 "p50glds 10M" "$O/p50glds_10m.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200 1,1g,0,0g
       cat "$O/p50glds_10m.txt"
       run 300 "p50glds 1.25M" "$O/p50glds_125.txt" python3 tools/diag/p50_top_ab.py 1250000 3 300 0,0g
       cat "$O/p50glds_125.txt" ;;
+    p50gldslib:*)
+      # the same A/B with another libbsr build (tools/ab/libbsr_<NAME>.so), e.g. the default-policy DMA
+      L="${step#*:}"
+      BSR_LIB=tools/ab/libbsr_$L.so run 400 "p50glds $L 10M" "$O/p50glds_${L}_10m.txt" python3 tools/diag/p50_top_ab.py 10000000 3 200 1,1g
+      cat "$O/p50glds_${L}_10m.txt" ;;
     gldstests)
-      BSR_SKINNY_GLDS=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+      BSR_SKINNY_GLDS=0 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
           tests/test_gpu_tiny_top.py tests/test_gpu_parity.py -k "tiny or small_batches or rescue or golden" \
           > "$O/gldstests.log" 2>&1
       rc=$?; echo "glds tests rc=$rc"; tail -3 "$O/gldstests.log"; [ $rc -eq 0 ] || exit $rc ;;
