@@ -1434,7 +1434,13 @@ hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     if (a.top_w && !(kp_on && a.n_items <= 16 && a.ld % 64 == 0 && a.ld <= 1024 && a.k <= 64 && a.kp <= 63 &&
                      4 * a.top_w <= 64u * kTopKeysPerLane))
         return hipErrorInvalidValue;  // (the self-thresholded path needs k_rescore_kp: the caller checks)
-    if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && a.n_items <= 16 && a.ld % 64 == 0 &&
+    // (lab, BSR_RESCORE_KP=2: the tiny-batch kernel for every batch size, for A/B runs)
+    static const bool kp_any = [] {
+        const char* v = getenv("BSR_RESCORE_KP");
+        return v && v[0] == '2';
+    }();
+    if (kp_on && a.sel && !a.n_items_dev && !a.pub_flag && !a.excl_out && (a.n_items <= 16 || kp_any) &&
+        a.ld % 64 == 0 &&
         a.ld <= 1024 && a.k <= 64 && a.kp <= 64 && (a.cap <= 1024 || a.top_w)) {
         hipLaunchKernelGGL(k_rescore_kp<1>, dim3(a.n_items), dim3(a.ld), 0, s, a);
         return hipGetLastError();

@@ -44,6 +44,7 @@
 #   gldstests   the single-query / small-batch tests with k_filter_skinny2 at 768-wide rows (BSR_SKINNY_GLDS=0)
 #   p50glds     p50 A/B of the LDS-DMA skinny filter against k_filter_skinny2 at 10M (self-thresholded and
 #               thresholded) and 1.25M (thresholded)
+#   kpab        the first rescore pass at 10M x 1000: one wave per query vs the tiny-batch kernel (BSR_RESCORE_KP=2)
 #   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
 #   rescue1     the single-query rescue case under the same switches (tools/diag/rescue1.py)
@@ -211,6 +212,16 @@ for step in $STEPS; do
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
+    kpab)
+      # the first rescore pass at 10M x 1000: the one-wave-per-query kernel (the product) against the
+      # tiny-batch kernel for every batch size (BSR_RESCORE_KP=2, lab), rocprof averages, interleaved
+      for r in 1 2; do
+        for v in 1 2; do
+          BSR_RESCORE_KP=$v run 300 "kp $v round $r" "$O/kpab_${v}_$r.json" rocprofv3 --kernel-trace --stats \
+              --output-format csv -d "$O/kpab_${v}_$r" -o run -- python3 bench.py --steps 10 --warmup 3 --verify 2 $NOB
+          python3 tools/diag/kstats.py "$O/kpab_${v}_$r" "$O/kpab_${v}_$r.json" rescore
+        done
+      done ;;
     seltauab)
       # tau0's selection at 10M x 1000 (9766 values per query): the 4-wave kernel (BSR_SELECT_TAU_M=1,
       # the product) against the 16-wave kernel (=2), rocprof averages, two interleaved rounds;
