@@ -363,6 +363,12 @@ def record_for_loopback(args):
     return path
 
 
+def skinny_kernel(nk):
+    """The skinny filter's row-mode kernel for rows of nk 64-byte K slices (csrc/k_filter.hip
+    launch_skinny: 768-byte rows take the LDS-DMA kernel unless BSR_SKINNY_GLDS=0)."""
+    return "k_filter_skinny_glds" if nk == 12 and os.environ.get("BSR_SKINNY_GLDS", "1")[:1] != "0" else "k_filter_skinny2"
+
+
 def main():
     args = parse()
     if args.config == "c1":
@@ -645,7 +651,7 @@ def main():
         if args.filter == "i8" and Q <= 16:
             # <= 16 queries on an int8 index: the skinny filter (HBM-bound)
             kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
-            kname = (f"k_filter_skinny2<{2 if st.search_path & bsr.BSR_PATH_SKINNY_TOP else 1}, {kv}>" if kv
+            kname = (f"{skinny_kernel(nk)}<{2 if st.search_path & bsr.BSR_PATH_SKINNY_TOP else 1}, {kv}>" if kv
                      else "k_filter_skinny<true>")
             sbytes = n_local * nk * 64
             gbs = sbytes / (emit_ms * 1e-3) / 1e9 if emit_ms > 0 else None
@@ -752,7 +758,7 @@ def main():
             if args.filter == "i8":
                 kv = next((c for c in (4, 8, 12, 16) if nk <= c), None)
                 mode = 2 if p50_path & bsr.BSR_PATH_SKINNY_TOP else 1  # (kSkTop / kSkEmit)
-                kbytes, kn = n_local * nk * 64, (f"k_filter_skinny2<{mode}, {kv}>" if kv else "k_filter_skinny<true>")
+                kbytes, kn = n_local * nk * 64, (f"{skinny_kernel(nk)}<{mode}, {kv}>" if kv else "k_filter_skinny<true>")
             else:
                 kbytes, kn = n_local * nk * 64 * 4, "k_scan_exact<1,1>"
             gbs = kbytes / (kms * 1e-3) / 1e9
