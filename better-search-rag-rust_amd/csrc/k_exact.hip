@@ -305,8 +305,10 @@ __device__ __forceinline__ bool put_result_rows(const RescoreArgs& a, uint32_t q
 __device__ uint64_t g_rescore_stamps[4096 * 8];
 #define BSR_STAMP(W_, I_)                                                                          \
     do {                                                                                           \
-        if ((W_) == 1 && (threadIdx.x & 63) == 0 && item < 4096)                                   \
+        if ((W_) == 1 && (threadIdx.x & 63) == 0 && item < 2048)                                   \
             g_rescore_stamps[item * 8 + (I_)] = __builtin_amdgcn_s_memrealtime();                  \
+        if ((W_) > 1 && threadIdx.x == 0 && item < 2048) /* (the second chance: slots 2048 +) */   \
+            g_rescore_stamps[(2048 + item) * 8 + (I_)] = __builtin_amdgcn_s_memrealtime();         \
     } while (0)
 #else
 #define BSR_STAMP(W_, I_) \
@@ -538,6 +540,9 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
         if (threadIdx.x == 0) s_last = solo || last_arrival(a.pub_ticket) ? 1u : 0u;
         __syncthreads();
         if (s_last) {
+#ifdef BSR_RESCORE_STAMPS
+            if (W > 1 && threadIdx.x == 0) g_rescore_stamps[4095 * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
             if (!solo) __threadfence();
             publish_copy(a.pub_src, a.pub_dst, a.pub_bytes, threadIdx.x, blockDim.x);
             __threadfence_system();
@@ -545,6 +550,9 @@ __global__ __launch_bounds__(64 * W * QPW) void k_rescore(RescoreArgs a) {
             if (threadIdx.x == 0) {
                 __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+#ifdef BSR_RESCORE_STAMPS
+            if (W > 1 && threadIdx.x == 0) g_rescore_stamps[4095 * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
     }
 }

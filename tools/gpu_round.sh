@@ -44,6 +44,7 @@
 #   gldstests   the single-query / small-batch tests with k_filter_skinny2 at 768-wide rows (BSR_SKINNY_GLDS=0)
 #   p50glds     p50 A/B of the LDS-DMA skinny filter against k_filter_skinny2 at 10M (self-thresholded and
 #               thresholded) and 1.25M (thresholded)
+#   scstamps    the second chance's phases at 10M x 1000 (tools/diag/second_chance_stamps.py, lab-stamps build)
 #   kpab        the first rescore pass at 10M x 1000: one wave per query vs the tiny-batch kernel (BSR_RESCORE_KP=2)
 #   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
 #   c3fb        the configs[3] searches' stats under the tiny-batch A/B switches (tools/diag/c3_fallback.py)
@@ -212,6 +213,11 @@ for step in $STEPS; do
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
+    scstamps)
+      # the second chance's phases at 10M x 1000 (lab stamps build, made beforehand)
+      BSR_LIB=tools/ab/libbsr_stamps.so run 300 "second-chance stamps" "$O/sc_stamps.txt" \
+          python3 tools/diag/second_chance_stamps.py 10000000
+      cat "$O/sc_stamps.txt" ;;
     kpab)
       # the first rescore pass at 10M x 1000: the one-wave-per-query kernel (the product) against the
       # tiny-batch kernel for every batch size (BSR_RESCORE_KP=2, lab), rocprof averages, interleaved
