@@ -438,16 +438,6 @@ static int filter_buffers(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k)
     BSR_TRY(ix->tau_excl.ensure((size_t)nq * sizeof(float)));
     BSR_TRY(ix->fail.ensure((size_t)nq * sizeof(uint32_t)));
     BSR_TRY(ix->fail2.ensure((size_t)nq * sizeof(uint32_t)));
-    if (nq > kSkinnyMaxQ && k <= 64 && rescore_sc_enabled()) {
-        // the grouped second chance's scratch: the groups' k best keys, the items' arrival
-        // counters (zero between launches: set once here, reset by each item's merging workgroup)
-        BSR_TRY(ix->sc_keys.ensure((size_t)qpad * kScGroups * k * sizeof(uint64_t)));
-        const size_t ab = (size_t)qpad * sizeof(uint32_t);
-        if (!ix->sc_arrive.p || ix->sc_arrive.bytes < ab) {
-            BSR_TRY(ix->sc_arrive.ensure(ab));
-            BSR_HIP(hipMemsetAsync(ix->sc_arrive.p, 0, ab, ix->stream));
-        }
-    }
     return BSR_OK;
 }
 
@@ -638,10 +628,6 @@ static int run_filter(bsr_index* ix, uint32_t nq, uint32_t qpad, uint32_t k, uin
     rb.tau0 = ix->tau.as<float>();
     rb.fail_cnt = status + kStFail2;
     rb.fail_list = ix->fail2.as<uint32_t>();
-    if (nq > kSkinnyMaxQ && k <= 64 && rescore_sc_enabled() && ix->sc_keys.p && ix->sc_arrive.p) {
-        rb.sc_keys = ix->sc_keys.as<uint64_t>();
-        rb.sc_arrive = ix->sc_arrive.as<uint32_t>();
-    }
     rb.next_status = next_status;
     rb.emit_cnt = ix->cnt.as<uint32_t>();
     rb.cur_status = status;

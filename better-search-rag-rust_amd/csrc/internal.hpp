@@ -87,8 +87,7 @@ struct bsr_index {
 
     // per-search scratch
     bsr::DevBuf q_in, qf32, nb, qop, qscale, ebound, qflags, tau, S, cand, cnt, cand_rows, ncand,
-        tau_excl, keys, fail, fail2, part, qids, qids_id, tmp,
-        sc_keys, sc_arrive;  // (the grouped second chance: the groups' keys, the items' counters)
+        tau_excl, keys, fail, fail2, part, qids, qids_id, tmp;
 
     // Packed per-search result, double-buffered: [status words | counts | distances |
     // indices].  One D2H copy per search reads it all back (into pinned memory); the

@@ -948,180 +948,6 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// The second chance of a batch (round 6): the queries that failed the first pass's certification
-// (their count read on the device), every row each emitted, certified against tau0 -- k_rescore
-// mode B's work and results, laid out as k_rescore_kp's.  An item's rows are cut into groups of 64,
-// and each group is one workgroup's unit: every wave loads its 64-float chunk of the group's rows
-// at once (one memory latency, not one per chunk), forms the rounded products and max|x_i - b_i| in
-// place, and the sequential sum walks the waves in chunk order through LDS -- the reference's
-// arithmetic in its order, so the bits of k_rescore.  Wave 0 keeps the group's k best keys
-// (sc_keys); the last group of an item to arrive (agent-scope release, counter, acquire) merges its
-// item's groups, certifies, and writes the result rows and the keys, as mode B does.  The grid is
-// persistent (units u = (item, group), blockIdx.x + j * gridDim.x); the launch publishes as
-// k_rescore does.
-// ------------------------------------------------------------------------------------
-template <int E>
-__global__ __launch_bounds__(768) void k_rescore_sc(RescoreArgs a) {  // (rows of <= 768 floats)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __shared__ __attribute__((aligned(16))) float stage[2 * kKpStage];
-    __shared__ float s_acc[64], s_mxw[16][64];
-    __shared__ uint32_t s_wrote;
-    const uint32_t n_items = *a.n_items_dev;
-    const uint32_t ld = a.ld, dim = a.dim, k = a.k, cap = a.cap;
-    if (threadIdx.x == 0) s_wrote = blockIdx.x == 0 ? 1u : 0u;
-    if (a.next_status && blockIdx.x == 0 && threadIdx.x < kWave) {
-        // (k_finalize's bookkeeping, fused: this is the batch's last kernel)
-        if (threadIdx.x < kStWords) a.next_status[threadIdx.x] = 0;
-        if (a.merge_words && threadIdx.x < 2) a.merge_words[threadIdx.x] = threadIdx.x ? ~0u : 0u;
-        uint32_t sum = 0;
-        for (uint32_t q = threadIdx.x; q < a.n_queries; q += kWave) sum += a.emit_cnt[q];
-        sum = wave_reduce_u32(sum, [](uint32_t x, uint32_t y) { return x + y; });
-        if (threadIdx.x == 0) a.cur_status[kStEmitted] = sum;
-    }
-    __syncthreads();
-    bool host_rows = false;  // (wave 0) this workgroup wrote result rows into the host mirror
-    const uint32_t units = n_items * kScGroups;
-    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint32_t f = u / kScGroups, g = u - f * kScGroups;
-        const uint32_t q = a.qlist[f];
-        const uint32_t cnt = a.cnt[q];
-        const bool overflow = cnt > cap;  // rows were dropped: nothing can be certified
-        const uint32_t c = overflow ? 0u : cnt;
-        const uint32_t ng = c ? (c + 63) / 64 : 1u;  // (an item with no rows: one empty group)
-        if (g >= ng) continue;  // (uniform)
-        // the group's rows (every wave reads the 64 keys itself) and this wave's query chunk
-        const uint32_t ci = g * 64 + lane;
-        const uint64_t ck = ci < c ? a.cand_keys[(uint64_t)q * cap + ci] : kKeyNone;
-        const bool valid = ck != kKeyNone;  // (an empty slot of a list: no row)
-        const uint32_t myrow = valid ? key_row(ck) : 0u;
-        uint32_t lrow[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) lrow[i] = (uint32_t)__shfl((int)myrow, (i * 64 + lane) >> 4, kWave);
-        f32x4_t pre[16];
-        load_cand_chunk(pre, a.rows, ld, lrow, (uint32_t)w, lane);
-        const uint32_t nvalid = dim > (uint32_t)w * 64 ? min(64u, dim - (uint32_t)w * 64) : 0u;
-        {
-            const uint32_t c0 = (lane & 15) * 4;
-            const f32x4_t bq = *reinterpret_cast<const f32x4_t*>(a.qf32 + (uint64_t)q * ld + w * 64 + c0);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                f32x4_t x = pre[i];
-                float m = 0.0f;
-                if (c0 + 0 < nvalid) m = fmaxf(m, fabsf(x.x - bq.x));
-                if (c0 + 1 < nvalid) m = fmaxf(m, fabsf(x.y - bq.y));
-                if (c0 + 2 < nvalid) m = fmaxf(m, fabsf(x.z - bq.z));
-                if (c0 + 3 < nvalid) m = fmaxf(m, fabsf(x.w - bq.w));
-                x.x = x.x * bq.x;
-                x.y = x.y * bq.y;
-                x.z = x.z * bq.z;
-                x.w = x.w * bq.w;
-                pre[i] = x;
-                m = fmaxf(m, __shfl_xor(m, 1, kWave));
-                m = fmaxf(m, __shfl_xor(m, 2, kWave));
-                m = fmaxf(m, __shfl_xor(m, 4, kWave));
-                m = fmaxf(m, __shfl_xor(m, 8, kWave));
-                if ((lane & 15) == 0) s_mxw[w][4 * i + (lane >> 4)] = m;
-            }
-        }
-        auto put = [&](float* st) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int L16 = i * 64 + lane;
-                *reinterpret_cast<f32x4_t*>(st + (L16 >> 4) * 68 + (L16 & 15) * 4) = pre[i];
-            }
-        };
-        if (w == 0) put(stage);
-        __syncthreads();
-        float acc = -0.0f;
-        for (int step = 0; step < nw; ++step) {
-            if (w == step) {
-                if (step) acc = s_acc[lane];
-                const float* my = stage + (step & 1) * kKpStage + lane * 68;
-                if (nvalid == 64) {
-#pragma unroll
-                    for (int i = 0; i < 64; i += 4) {
-                        const f32x4_t x = *reinterpret_cast<const f32x4_t*>(my + i);
-                        acc = acc + x.x;
-                        acc = acc + x.y;
-                        acc = acc + x.z;
-                        acc = acc + x.w;
-                    }
-                } else {
-                    for (uint32_t i = 0; i < nvalid; ++i) acc = acc + my[i];
-                }
-                s_acc[lane] = acc;
-            } else if (w == step + 1) {
-                put(stage + (w & 1) * kKpStage);
-            }
-            __syncthreads();
-        }
-        if (w == 0) {
-            const float mag_b = a.nb[q];
-            WaveTopK<E> L;
-            L.init();
-            uint64_t thr = kKeyNone;
-            {
-                float mx = 0.0f;
-                for (int v = 0; v < nw; ++v) mx = fmaxf(mx, s_mxw[v][lane]);
-                const float d = finish_distance(s_acc[lane], mx, a.na[myrow], mag_b);  // (the last wave's sum)
-                L.offer(valid ? dist_key(d, myrow) : kKeyNone, (int)k, thr);
-            }
-            uint64_t* const gk = a.sc_keys + (uint64_t)f * kScGroups * k;
-            L.store(gk + (uint64_t)g * k, (int)k);
-            // the item's last group to arrive merges (release: this wave's keys; acquire: theirs)
-            __threadfence();
-            uint32_t old = 0;
-            if (lane == 0) old = atomicAdd(a.sc_arrive + f, 1u);
-            if ((uint32_t)__shfl((int)old, 0, kWave) == ng - 1) {
-                __threadfence();
-                WaveTopK<E> M;
-                M.init();
-                uint64_t mt = kKeyNone;
-                for (uint32_t gg = 0; gg < ng; ++gg)
-                    for (uint32_t b = 0; b < k; b += kWave)
-                        M.offer(b + lane < k ? gk[(uint64_t)gg * k + b + lane] : kKeyNone, (int)k, mt);
-                if (lane == 0) a.sc_arrive[f] = 0u;  // (for the next launch)
-                M.store(a.out_keys + (uint64_t)q * k, (int)k);
-                bool failed = false;
-                if (lane == 0) {
-                    // (mode B: every emitted row is a candidate, so tau_x is the emission threshold)
-                    const bool ok = certify(overflow ? INFINITY : a.tau0[q], mt, a.ebound[q], mag_b);
-                    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1u)] = q;
-                    failed = !ok;
-                }
-                if (__shfl((int)failed, 0, kWave)) s_wrote = 1u;
-                if (a.res_idx)
-                    host_rows = put_result_rows(a, q, M, (uint64_t)k < a.n_rows ? k : (uint32_t)a.n_rows, lane) ||
-                                host_rows;
-            }
-        }
-        __syncthreads();  // (the stage and s_acc are the next unit's)
-    }
-    if (a.pub_flag) {
-        // publish, as k_rescore (never solo: tiny batches keep k_rescore's one-workgroup grid)
-        __shared__ uint32_t s_last;
-        __syncthreads();  // (s_wrote final)
-        if (s_wrote || !a.hres_idx) __threadfence();
-        if (BSR_PUB_SYSREL && __ballot(host_rows)) release_system();  // (wave 0 wrote them)
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) s_last = last_arrival(a.pub_ticket) ? 1u : 0u;
-        __syncthreads();
-        if (s_last) {
-            __threadfence();
-            publish_copy(a.pub_src, a.pub_dst, a.pub_bytes, threadIdx.x, blockDim.x);
-            __threadfence_system();
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(a.pub_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-    } else if (BSR_PUB_SYSREL && __ballot(host_rows)) {
-        release_system();
-    }
-}
-
-// ------------------------------------------------------------------------------------
 // Exact full scan (src/mpi_helpers/metrics.rs:36-50 for up to QF queries at once): 256
 // rows per tile (lane = row), 64-element chunks of the row-major slab staged through LDS
 // (padded to 68 floats: conflict-free ds_read_b128), next chunk prefetched into registers.
@@ -1604,14 +1430,6 @@ bool rescore_kp_enabled() {
     const char* v = getenv("BSR_RESCORE_KP");
     return !(v && v[0] == '0');
 }
-// (lab for now: BSR_SC_GROUPS=1 -- the grouped second chance, read once per process)
-bool rescore_sc_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("BSR_SC_GROUPS");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
 
 hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     if (!a_in.n_items) return hipSuccess;
@@ -1661,12 +1479,6 @@ hipError_t launch_rescore(const RescoreArgs& a_in, hipStream_t s) {
     }
     // items counted on the device: a persistent grid of 8-wave workgroups; else one wave per item
     const bool dev = a.n_items_dev != nullptr;
-    // (batches of > 16 queries: the grouped second chance, one workgroup per 64 rows of an item)
-    if (dev && a.sc_keys && a.sc_arrive && a.cand_keys && !a.excl_out && a.n_items > 16 && a.ld % 64 == 0 &&
-        a.ld <= 768 && a.k <= 64 && a.cap <= kScGroups * 64 && rescore_sc_enabled()) {
-        hipLaunchKernelGGL(k_rescore_sc<1>, dim3(kRescoreAllGrid), dim3(a.ld), 0, s, a);
-        return hipGetLastError();
-    }
     // (one item per wave: four independent waves per workgroup, one workgroup per CU)
     // (a tiny batch's second chance: one workgroup, its own last arrival -- rarely any item)
     // (BSR_SOLO_PUB=0: the grid as before, for A/B runs)

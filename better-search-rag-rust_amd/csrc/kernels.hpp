@@ -238,14 +238,7 @@ struct RescoreArgs {
     uint32_t* pub_flag;
     uint32_t* pub_ticket;       // kTicketWords device words, 0 between launches
     uint32_t solo;              // (set by launch_rescore) a one-workgroup grid: its own last arrival
-    // (the grouped second chance, k_rescore_sc) each item's rows in groups of 64, one workgroup
-    // per group: the groups' k best keys [item][kScGroups][k] and the items' arrival counters
-    // (zero between launches; the merging workgroup resets its own)
-    uint64_t* sc_keys;
-    uint32_t* sc_arrive;
 };
-// Groups of 64 rows per second-chance item (cap <= 1024 emitted keys)
-constexpr uint32_t kScGroups = 16;
 // The publishing kernels' arrival ticket: kTicketLeaves leaf counters and one root counter,
 // each on a 64-byte line of its own (a workgroup adds to its leaf, blockIdx % kTicketLeaves; the
 // last of a leaf adds to the root), all zero between launches.
@@ -257,7 +250,6 @@ constexpr uint32_t kFusedSelectCap = 1024;
 hipError_t launch_rescore(const RescoreArgs& a, hipStream_t s);
 // whether launch_rescore takes k_rescore_kp for a tiny batch's first pass (BSR_RESCORE_KP != 0)
 bool rescore_kp_enabled();
-bool rescore_sc_enabled();  // the grouped second chance for batches of > 16 queries (k_rescore_sc)
 // The self-thresholded path's lists per query are selected by one wave, this many keys per lane.
 constexpr uint32_t kTopKeysPerLane = 32;
 // Exact full scan for up to kScanQF queries (ids in qids, device).  part must hold

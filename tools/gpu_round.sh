@@ -44,7 +44,6 @@
 #   gldstests   the single-query / small-batch tests with k_filter_skinny2 at 768-wide rows (BSR_SKINNY_GLDS=0)
 #   p50glds     p50 A/B of the LDS-DMA skinny filter against k_filter_skinny2 at 10M (self-thresholded and
 #               thresholded) and 1.25M (thresholded)
-#   scab        the grouped second chance (BSR_SC_GROUPS=1, lab): its GPU tests, then a rocprof A/B at 10M x 1000
 #   scstamps    the second chance's phases at 10M x 1000 (tools/diag/second_chance_stamps.py, lab-stamps build)
 #   kpab        the first rescore pass at 10M x 1000: one wave per query vs the tiny-batch kernel (BSR_RESCORE_KP=2)
 #   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
@@ -214,19 +213,6 @@ for step in $STEPS; do
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
-    scab)
-      # the grouped second chance (BSR_SC_GROUPS=1, lab) against k_rescore's 8-wave item: its tests, then
-      # rocprof averages of the default bench, interleaved (kernel names: k_rescore<1, 8, 2, 1> / k_rescore_sc)
-      BSR_SC_GROUPS=1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-          tests/test_gpu_parity.py tests/test_gpu_random_sweep.py > "$O/sc_tests.log" 2>&1
-      rc=$?; echo "sc tests rc=$rc"; tail -2 "$O/sc_tests.log"; [ $rc -eq 0 ] || exit $rc
-      for r in 1 2; do
-        for v in 0 1; do
-          BSR_SC_GROUPS=$v run 300 "sc $v round $r" "$O/scab_${v}_$r.json" rocprofv3 --kernel-trace --stats \
-              --output-format csv -d "$O/scab_${v}_$r" -o run -- python3 bench.py --steps 10 --warmup 3 --verify 2 $NOB
-          python3 tools/diag/kstats.py "$O/scab_${v}_$r" "$O/scab_${v}_$r.json" "k_rescore<1, 8" k_rescore_sc "k_rescore<1, 1"
-        done
-      done ;;
     scstamps)
       # the second chance's phases at 10M x 1000 (lab stamps build, made beforehand)
       BSR_LIB=tools/ab/libbsr_stamps.so run 300 "second-chance stamps" "$O/sc_stamps.txt" \
