@@ -181,3 +181,34 @@ def test_top_path_other_widths(bsr_mod, oracle_mod, gpu, dim, nq, k):
         _same(got, want, f"dim {dim} nq {nq} k {k} rep {rep}")
     assert got[0][0, 0] == n - 1 and got[1][0, 0] == 0.0
     ix.close()
+
+
+@pytest.mark.parametrize("top", ["1", "0"])
+def test_top_path_bf16_corpus(bsr_mod, oracle_mod, gpu, monkeypatch, top):
+    """configs[4]'s corpus type on the single-query paths: a bf16 corpus (widened exactly to f32 at
+    load; the reference's values are the widened ones) of 2.2M rows, 768 wide -- the LDS-DMA skinny
+    filter in both row modes (self-thresholded and thresholded) -- with a planted self-match:
+    bit-exact against the oracle over the widened rows."""
+    import torch
+    n, dim, nq, k = 2_200_011, 768, 4, 10
+    rows = torch.empty((n, dim), dtype=torch.float32, device="cuda:0")
+    bsr_mod.synth_uniform(rows.data_ptr(), 0, n, dim, 21)
+    rows16 = rows.to(torch.bfloat16)
+    del rows
+    q = rows16[[7, n // 2, n - 1, 12345]].float()
+    q[3] = q[3] * 0.5 + 0.25
+    torch.cuda.synchronize()
+    ix = bsr_mod.Index(dim, max_k=64, device=0, dtype=bsr_mod.BSR_BF16)
+    ix.load(rows16)
+    host = rows16.float().cpu().numpy()
+    del rows16
+    torch.cuda.empty_cache()
+    qh = np.ascontiguousarray(q.cpu().numpy())
+    want = oracle_mod.parallel_top_k(host, qh, k, size=THREADS, threads=THREADS)
+    monkeypatch.setenv("BSR_SKINNY_TOP", top)
+    for rep in range(2):
+        got = ix.local_top_k(qh, k)
+        assert bool(ix.last_stats().search_path & bsr_mod.BSR_PATH_SKINNY_TOP) == (top == "1")
+        _same(got, want, f"bf16 top={top} rep {rep}")
+    assert list(got[0][:3, 0]) == [7, n // 2, n - 1]
+    ix.close()
