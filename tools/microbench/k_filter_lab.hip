@@ -1,5 +1,5 @@
 // k_filter_lab.hip -- TOOLING: the MFMA filter with its ablation knobs (VAR / STAG / PRIO /
-// EPI / STAMP) for tools/microbench/gemm_ablate; the product kernel is
+// EPI / STAMP), included by tools/microbench/ring_ab; the product kernel is
 // better-search-rag-rust_amd/csrc/k_filter.hip (no knobs).  Round-1 snapshot.
 //
 // The filter scores every (corpus row, query) pair approximately on the matrix cores and
