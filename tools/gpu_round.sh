@@ -17,6 +17,8 @@
 #   rehprof     rocprofv3 kernel stats of the --gpus 8 host rehearsal (every rank process traced)
 #   stamps      s_memtime phase split of the emit filter (make lab-fstamps) at 10M and 1.25M
 #   counters    emission-epilogue event counts + per-workgroup balance (make lab-counters)
+#   (the lab binaries these steps run are built here beforehand -- make -C tools/microbench filter_ab
+#    filter_hist ... -- and are git-ignored; the tree holds their sources only)
 #   fab         tools/microbench/filter_ab (product vs variants of the emit filter) at 10M and 1.25M
 #   fabshard    filter_ab at the rank shards of N = 2, 4, 8 (5M, 2.5M, 1.25M rows) at the global threshold's
 #               emission rate (tau 0.1473: ~256 rows per query over the 10M corpus, 256/N per rank)
