@@ -729,6 +729,9 @@ __device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uin
         mx = ((uint64_t)hi << 32) | lo;
     }
     const uint64_t X = mx;
+#ifdef BSR_RESCORE_STAMPS
+    if (lane == 0 && q < 2048) g_rescore_stamps[q * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // (keys in, X)
+#endif
     const float tx_trunc = X == kKeyNone ? -INFINITY : score_key_score(X);
     // the second chance's input first (select_kp compacts in place): the keys below X, in order
     uint32_t base = 0;
@@ -765,6 +768,9 @@ __device__ __forceinline__ void top_select(const RescoreArgs& a, uint32_t q, uin
     }
     if (nl <= 8 * kWave && nh >= K) {
         const uint64_t H = kth_key<8>(hv, K, ~0u);
+#ifdef BSR_RESCORE_STAMPS
+        if (lane == 0 && q < 2048) g_rescore_stamps[q * 8 + 7] = __builtin_amdgcn_s_memrealtime();  // (H)
+#endif
         uint64_t* const cb = scratch + 8 * kWave;
         uint32_t C = 0;
 #pragma unroll

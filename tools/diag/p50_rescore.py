@@ -60,10 +60,12 @@ if os.environ.get("BSR_READ_STAMPS") == "1":
     st = np.zeros((4096, 8), np.uint64)
     L.bsr_lab_rescore_stamps.restype = ctypes.c_int
     assert L.bsr_lab_rescore_stamps(st.ctypes.data_as(ctypes.c_void_p), 4096) == 0
-    s = st[:Q, :6].astype(np.int64)
+    s = st[:Q, :8].astype(np.int64)
     us = (s - s[:, :1]) / 100.0
-    for nm, i, j in (("keys arrive", 5, 0), ("select", 1, 5), ("rows -> LDS", 2, 1), ("walk chunks", 3, 2),
-                     ("finish", 4, 3)):
+    phases = [("keys arrive", 5, 0), ("select", 1, 5), ("rows -> LDS", 2, 1), ("walk chunks", 3, 2), ("finish", 4, 3)]
+    if s[0, 6] and s[0, 7]:  # (the self-thresholded path: the selection's own stamps)
+        phases[1:2] = [("  keys in, X", 6, 5), ("  lists, heads, H", 7, 6), ("  candidates", 1, 7)]
+    for nm, i, j in phases:
         d = us[:, i] - us[:, j]
         print(f"  {nm:16s} median {np.median(d):7.2f} max {d.max():7.2f} us", flush=True)
     print(f"  {'total':16s} median {np.median(us[:, 4]):7.2f} max {us[:, 4].max():7.2f} us", flush=True)
