@@ -19,10 +19,7 @@
 #ifndef BSR_PUB_SYSREL
 #define BSR_PUB_SYSREL 1
 #endif
-// (lab) the tiny-batch rescore's other waves touch the list heads' rows while wave 0 selects
-#ifndef BSR_KP_PREFETCH
-#define BSR_KP_PREFETCH 0
-#endif
+
 
 namespace {
 // A system-scope release of this wave's prior stores (buffer_wbl2 sc0 sc1 + the wait), then the
@@ -818,9 +815,6 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
     __shared__ uint32_t lsel[64];
     __shared__ uint32_t s_c, s_ov;
     __shared__ float s_tx;
-#if BSR_KP_PREFETCH
-    __shared__ uint32_t s_touch[64];  // (lab: the row touches' sink)
-#endif
     const uint32_t item = blockIdx.x;
     if (item >= a.n_items) return;  // (grid = n_items: uniform per workgroup)
     if (w == 0) BSR_STAMP(1, 0);
@@ -835,27 +829,6 @@ __global__ __launch_bounds__(1024) void k_rescore_kp(RescoreArgs a) {
             top_select(a, q, lsel, s_c, s_tx, s_ov, lane, reinterpret_cast<uint64_t*>(stage));
             BSR_STAMP(1, 1);
         }
-#if BSR_KP_PREFETCH
-        else {
-            // (lab) while wave 0 selects, the other waves touch their chunk (wave 1: chunk 0 too) of
-            // every list head's row, so that the candidates' loads below hit L2 -- the k' candidates
-            // are nearly all list heads
-            const uint64_t* const list = a.cand_keys + (uint64_t)q * a.cap;
-            for (uint32_t i = lane; i < a.top_w; i += kWave) {
-                const uint64_t key = list[4 * i];
-                if (key == kKeyNone) continue;
-                const float* const r = a.rows + (uint64_t)key_row(key) * ld + w * 64;
-                // (LDS-DMA into a scratch line nobody reads: no register is written behind the
-                // compiler's back)
-                __builtin_amdgcn_global_load_lds((const void*)r, (lds_void_t*)s_touch, 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(r + 32), (lds_void_t*)s_touch, 4, 0, 0);
-                if (w == 1) {
-                    __builtin_amdgcn_global_load_lds((const void*)(r - 64), (lds_void_t*)s_touch, 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const void*)(r - 32), (lds_void_t*)s_touch, 4, 0, 0);
-                }
-            }
-        }
-#endif
     } else if (w == 0) {
         constexpr int NR = 16;
         uint64_t xk[NR];
