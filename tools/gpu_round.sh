@@ -46,6 +46,7 @@
 #   gldstests   the single-query / small-batch tests with k_filter_skinny2 at 768-wide rows (BSR_SKINNY_GLDS=0)
 #   p50glds     p50 A/B of the LDS-DMA skinny filter against k_filter_skinny2 at 10M (self-thresholded and
 #               thresholded) and 1.25M (thresholded)
+#   p50api      the host's HIP API calls between single-query searches (rocprofv3 --hip-trace, tools/diag/api_gap.py)
 #   scstamps    the second chance's phases at 10M x 1000 (tools/diag/second_chance_stamps.py, lab-stamps build)
 #   kpab        the first rescore pass at 10M x 1000: one wave per query vs the tiny-batch kernel (BSR_RESCORE_KP=2)
 #   seltauab    tau0's selection at 10M x 1000: the 4-wave kernel vs the 16-wave one (BSR_SELECT_TAU_M=2)
@@ -215,6 +216,12 @@ for step in $STEPS; do
     r125)
       run 300 "bench 1.25M" "$O/bench_125.json" python bench.py --rows 1250000 --steps 30 --warmup 3 --verify 2 $NOB
       head -c 400 "$O/bench_125.json"; echo ;;
+    p50api)
+      # the host's share of the single-query search: HIP API calls between one search's last kernel
+      # and the next one's query prep (rocprofv3 HIP API + kernel trace of tools/diag/p50_rescore.py)
+      run 300 "p50 api trace" "$O/p50api.txt" rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$O/p50api" \
+          -o run -- python3 tools/diag/p50_rescore.py ${P50ROWS:-10000000} 1
+      python3 tools/diag/api_gap.py "$O/p50api" "k_rescore<1, 8, 2, 1>" > "$O/api_gap_p50.txt"; cat "$O/api_gap_p50.txt" ;;
     scstamps)
       # the second chance's phases at 10M x 1000 (lab stamps build, made beforehand)
       BSR_LIB=tools/ab/libbsr_stamps.so run 300 "second-chance stamps" "$O/sc_stamps.txt" \
